@@ -1,0 +1,8 @@
+"""cmpc -- MI355X-native batched convex-MPC contact-force QP solver.
+
+Drop-in for the CasADi/OSQP solve of ltinphan/convex-mpc-unitree-go2
+(convex_mpc/centroidal_mpc.py).  See DESIGN.md.
+"""
+from .solver import Plan, SolverParams, CmpcError, solve_batch, to_device_batch, STATUS_STRINGS  # noqa: F401
+
+__version__ = "0.1.0"

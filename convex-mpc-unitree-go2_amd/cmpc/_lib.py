@@ -1,0 +1,76 @@
+"""ctypes binding of the C-ABI declared in ``include/cmpc.h``.
+
+This is the Python side of the drop-in boundary: the reference calls CasADi's conic/OSQP
+plugin from Python (``centroidal_mpc.py:212-213, 98``); here Python calls ``libcmpc.so``.
+The product path has no CPU fallback: if the library is missing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+from .build import LIB
+
+ABI_VERSION = 1
+CMPC_OK = 0
+
+
+class CParams(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("N", ctypes.c_int32),
+        ("Q", ctypes.c_float * 12),
+        ("R", ctypes.c_float * 12),
+        ("mu", ctypes.c_float),
+        ("fz_min", ctypes.c_float),
+        ("eps_abs", ctypes.c_float),
+        ("eps_rel", ctypes.c_float),
+        ("max_iter", ctypes.c_int32),
+        ("rho", ctypes.c_float),
+        ("sigma", ctypes.c_float),
+        ("alpha", ctypes.c_float),
+        ("adaptive_rho_interval", ctypes.c_int32),
+        ("polish_stable", ctypes.c_int32),
+        ("polish_refine", ctypes.c_int32),
+        ("polish_tol", ctypes.c_float),
+        ("max_batch", ctypes.c_int64),
+    ]
+
+
+EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
+           "cmpc_last_error", "cmpc_version")
+
+_lib = None
+
+
+def load(path: str | Path | None = None) -> ctypes.CDLL:
+    """Load libcmpc.so (in-tree) and declare the prototypes.  Raises if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path is not None else LIB
+    if not p.exists():
+        raise RuntimeError(f"cmpc: HIP library {p} not built (run __graft_entry__.build() or "
+                           f"python -m cmpc.build); there is no CPU fallback")
+    lib = ctypes.CDLL(str(p))
+    vp = ctypes.c_void_p
+    lib.cmpc_params_default.argtypes = [ctypes.POINTER(CParams)]
+    lib.cmpc_params_default.restype = None
+    lib.cmpc_plan_create.argtypes = [ctypes.POINTER(CParams), ctypes.POINTER(vp)]
+    lib.cmpc_plan_create.restype = ctypes.c_int
+    lib.cmpc_solve.argtypes = [vp, ctypes.c_int64] + [vp] * 10
+    lib.cmpc_solve.restype = ctypes.c_int
+    lib.cmpc_plan_destroy.argtypes = [vp]
+    lib.cmpc_plan_destroy.restype = None
+    lib.cmpc_last_error.argtypes = []
+    lib.cmpc_last_error.restype = ctypes.c_char_p
+    lib.cmpc_version.argtypes = []
+    lib.cmpc_version.restype = ctypes.c_char_p
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def last_error(lib=None) -> str:
+    lib = lib or load()
+    return lib.cmpc_last_error().decode()

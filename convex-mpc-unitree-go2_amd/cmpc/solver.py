@@ -1,0 +1,160 @@
+"""Batched solver on device tensors: the C-ABI wrapped for PyTorch-ROCm buffers.
+
+``Plan`` mirrors what ``CentroidalMPC.__init__`` builds once (``centroidal_mpc.py:41-67``:
+constants, sparsity, solver object); ``Plan.solve`` is the batched equivalent of
+``solve_QP``'s update + solve (``centroidal_mpc.py:69-120``).  PyTorch is used only for device
+memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field, fields
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+STATUS_STRINGS = {1: "solved", 2: "solved inaccurate", -2: "maximum iterations reached",
+                  -10: "unsolved"}
+
+
+@dataclass
+class SolverParams:
+    """cmpc_params (include/cmpc.h).  Defaults = the reference's constants
+    (centroidal_mpc.py:12-38, :127) plus this solver's ADMM/polish settings."""
+    N: int = 16
+    Q: tuple = (1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1)
+    R: tuple = (1e-5,) * 12
+    mu: float = 0.8
+    fz_min: float = 10.0
+    eps_abs: float = 1e-4
+    eps_rel: float = 1e-4
+    max_iter: int = 1000
+    rho: float = 1e-4
+    sigma: float = 1e-6
+    alpha: float = 1.6
+    adaptive_rho_interval: int = 25
+    polish_stable: int = 3
+    polish_refine: int = 4
+    polish_tol: float = 1e-5
+    max_batch: int = 65536
+
+    def to_c(self) -> _lib.CParams:
+        c = _lib.CParams()
+        c.abi_version = _lib.ABI_VERSION
+        for f in fields(self):
+            val = getattr(self, f.name)
+            if f.name in ("Q", "R"):
+                if len(val) != 12:
+                    raise ValueError(f"{f.name} must have 12 entries")
+                setattr(c, f.name, (ctypes.c_float * 12)(*[float(v) for v in val]))
+            else:
+                setattr(c, f.name, val)
+        return c
+
+
+class CmpcError(RuntimeError):
+    pass
+
+
+def _check(lib, rc: int, what: str):
+    if rc != _lib.CMPC_OK:
+        raise CmpcError(f"{what} failed ({rc}): {_lib.last_error(lib)}")
+
+
+def _dev_tensor(t: torch.Tensor, name: str, dtype, shape) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a device (cuda/ROCm) tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)}, got {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+class Plan:
+    """Owns a cmpc_plan (device workspace for up to params.max_batch instances)."""
+
+    def __init__(self, params: Optional[SolverParams] = None, device=None):
+        self.params = params or SolverParams()
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise CmpcError("cmpc: no ROCm device available (the solver has no CPU fallback)")
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else torch.device(device).index or 0)
+        with torch.cuda.device(self.device):
+            h = ctypes.c_void_p()
+            cp = self.params.to_c()
+            _check(self.lib, self.lib.cmpc_plan_create(ctypes.byref(cp), ctypes.byref(h)),
+                   "cmpc_plan_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.cmpc_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def solve(self, Ad, Bd, gd, x0, xref, contact, out=None, stream=None):
+        """Solve B instances; all inputs are device tensors (layouts: include/cmpc.h).
+
+        Returns (w (B, 24N) fp32, status (B,) int32, iters (B,) int32).  Asynchronous on
+        ``stream`` (default: torch's current stream)."""
+        N = self.params.N
+        B = Ad.shape[0]
+        f32 = torch.float32
+        _dev_tensor(Ad, "Ad", f32, (B, 12, 12))
+        _dev_tensor(Bd, "Bd", f32, (B, N, 12, 12))
+        _dev_tensor(gd, "gd", f32, (B, 12))
+        _dev_tensor(x0, "x0", f32, (B, 12))
+        _dev_tensor(xref, "xref", f32, (B, N, 12))
+        _dev_tensor(contact, "contact", torch.uint8, (B, 4, N))
+        for t in (Bd, gd, x0, xref, contact):
+            if t.device != Ad.device:
+                raise ValueError("all inputs must be on the same device")
+        if out is None:
+            w = torch.empty((B, 24 * N), dtype=f32, device=Ad.device)
+            status = torch.empty((B,), dtype=torch.int32, device=Ad.device)
+            iters = torch.empty((B,), dtype=torch.int32, device=Ad.device)
+        else:
+            w, status, iters = out
+            _dev_tensor(w, "w", f32, (B, 24 * N))
+            _dev_tensor(status, "status", torch.int32, (B,))
+            _dev_tensor(iters, "iters", torch.int32, (B,))
+        if stream is None:
+            stream = torch.cuda.current_stream(Ad.device)
+        sp = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        with torch.cuda.device(Ad.device):
+            rc = self.lib.cmpc_solve(self._h, ctypes.c_int64(B), *[ctypes.c_void_p(t.data_ptr())
+                                     for t in (Ad, Bd, gd, x0, xref, contact, w, status, iters)],
+                                     sp)
+        _check(self.lib, rc, "cmpc_solve")
+        return w, status, iters
+
+
+def to_device_batch(batch: dict, device="cuda") -> dict:
+    """float64/uint8 numpy batch (cmpc.synth layout) -> contiguous device tensors."""
+    out = {}
+    for k in ("Ad", "Bd", "gd", "x0", "xref"):
+        out[k] = torch.as_tensor(batch[k], dtype=torch.float32).contiguous().to(device)
+    out["contact"] = torch.as_tensor(batch["contact"], dtype=torch.uint8).contiguous().to(device)
+    return out
+
+
+def solve_batch(batch: dict, params: Optional[SolverParams] = None, plan: Optional[Plan] = None):
+    """Convenience: numpy batch in, (w, status, iters) numpy out (synchronises)."""
+    plan = plan or Plan(params)
+    d = to_device_batch(batch, plan.device)
+    w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+    torch.cuda.synchronize(plan.device)
+    return w.cpu().numpy(), st.cpu().numpy(), it.cpu().numpy()

@@ -1,0 +1,42 @@
+// cmpc_device.h -- device-side parameter block shared by the kernels and the host launcher.
+#pragma once
+#include <stdint.h>
+
+namespace cmpc {
+
+// Kernel-argument copy of cmpc_params with the reference's factor 2 folded in
+// (H = diag(2Q, 2R), centroidal_mpc.py:178-201).
+struct KParams {
+  int N;
+  float Q2[12];
+  float R2[12];
+  float mu, fz_min;
+  float rho0, sigma, alpha;
+  float eps_abs, eps_rel;
+  float polish_tol;
+  int max_iter;
+  int adaptive_interval;
+  int polish_stable;
+  int polish_refine;
+};
+
+// Device pointers of one cmpc_solve call (layouts: include/cmpc.h).
+struct Inputs {
+  const float* Ad;
+  const float* Bd;
+  const float* gd;
+  const float* x0;
+  const float* xref;
+  const uint8_t* contact;
+};
+struct Outputs {
+  float* w;
+  int32_t* status;
+  int32_t* iters;
+};
+
+// Free-variable capacities of the LDS bins (3 forces per stance (step, leg)).
+constexpr int kNumBins = 4;
+constexpr int kBinCap[kNumBins] = {96, 128, 160, 192};
+
+}  // namespace cmpc

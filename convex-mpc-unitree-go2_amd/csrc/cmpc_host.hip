@@ -1,0 +1,189 @@
+// cmpc_host.hip -- C-ABI (include/cmpc.h): plan management and kernel launches.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+#include <string>
+
+#include "cmpc.h"
+#include "cmpc_device.h"
+
+#include "cmpc_kernels.hip"  // kernels: same translation unit
+
+struct cmpc_plan {
+  cmpc_params p;
+  cmpc::KParams kp;
+  int device;
+  int* d_counters;  // counts[kNumBins], heads[kNumBins]
+  int* d_lists;     // kNumBins * max_batch
+  int grid[cmpc::kNumBins];
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(CMPC_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+using KernelFn = void (*)(cmpc::KParams, cmpc::Inputs, cmpc::Outputs, const int*, const int*,
+                          int*);
+
+KernelFn bin_fn(int q) {
+  switch (q) {
+    case 0: return cmpc::solve_bin_kernel<96>;
+    case 1: return cmpc::solve_bin_kernel<128>;
+    case 2: return cmpc::solve_bin_kernel<160>;
+    default: return cmpc::solve_bin_kernel<192>;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+void cmpc_params_default(cmpc_params* p) {
+  if (!p) return;
+  memset(p, 0, sizeof(*p));
+  p->abi_version = CMPC_ABI_VERSION;
+  p->N = 16;
+  const float Q[12] = {1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1};  // centroidal_mpc.py:12
+  for (int i = 0; i < 12; ++i) {
+    p->Q[i] = Q[i];
+    p->R[i] = 1e-5f;  // centroidal_mpc.py:13
+  }
+  p->mu = 0.8f;        // centroidal_mpc.py:15
+  p->fz_min = 10.f;    // centroidal_mpc.py:127
+  p->eps_abs = 1e-4f;  // centroidal_mpc.py:25-26
+  p->eps_rel = 1e-4f;
+  p->max_iter = 1000;  // centroidal_mpc.py:27
+  p->rho = 1e-4f;
+  p->sigma = 1e-6f;    // OSQP default
+  p->alpha = 1.6f;     // OSQP default
+  p->adaptive_rho_interval = 25;  // centroidal_mpc.py:32
+  p->polish_stable = 3;
+  p->polish_refine = 4;
+  p->polish_tol = 1e-5f;
+  p->max_batch = 65536;
+}
+
+int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
+  if (!p || !out) return fail(CMPC_E_INVALID, "cmpc_plan_create: null argument");
+  *out = nullptr;
+  if (p->abi_version != CMPC_ABI_VERSION)
+    return fail(CMPC_E_INVALID, "cmpc_plan_create: abi_version mismatch");
+  if (p->N < 1 || p->N > 16) return fail(CMPC_E_INVALID, "cmpc_plan_create: N must be in 1..16");
+  for (int i = 0; i < 12; ++i) {
+    if (!(p->Q[i] >= 0.f) || !std::isfinite(p->Q[i]))
+      return fail(CMPC_E_INVALID, "cmpc_plan_create: Q must be finite and >= 0");
+    if (!(p->R[i] > 0.f) || !std::isfinite(p->R[i]))
+      return fail(CMPC_E_INVALID, "cmpc_plan_create: R must be finite and > 0");
+  }
+  if (!(p->mu > 0.f) || !std::isfinite(p->mu)) return fail(CMPC_E_INVALID, "cmpc_plan_create: mu must be > 0");
+  if (!std::isfinite(p->fz_min)) return fail(CMPC_E_INVALID, "cmpc_plan_create: fz_min must be finite");
+  if (p->max_iter < 1) return fail(CMPC_E_INVALID, "cmpc_plan_create: max_iter must be >= 1");
+  if (!(p->rho > 0.f) || !(p->sigma >= 0.f) || !(p->alpha > 0.f && p->alpha < 2.f))
+    return fail(CMPC_E_INVALID, "cmpc_plan_create: need rho > 0, sigma >= 0, 0 < alpha < 2");
+  if (p->polish_stable < 1 || p->polish_refine < 1 || !(p->polish_tol > 0.f))
+    return fail(CMPC_E_INVALID, "cmpc_plan_create: polish settings out of range");
+  if (p->adaptive_rho_interval < 0 || p->max_batch < 1 || p->max_batch > (1LL << 30))
+    return fail(CMPC_E_INVALID, "cmpc_plan_create: adaptive_rho_interval/max_batch out of range");
+
+  cmpc_plan* pl = new cmpc_plan();
+  pl->p = *p;
+  cmpc::KParams& k = pl->kp;
+  k.N = p->N;
+  for (int i = 0; i < 12; ++i) {
+    k.Q2[i] = 2.f * p->Q[i];
+    k.R2[i] = 2.f * p->R[i];
+  }
+  k.mu = p->mu;
+  k.fz_min = p->fz_min;
+  k.rho0 = p->rho;
+  k.sigma = p->sigma;
+  k.alpha = p->alpha;
+  k.eps_abs = p->eps_abs;
+  k.eps_rel = p->eps_rel;
+  k.polish_tol = p->polish_tol;
+  k.max_iter = p->max_iter;
+  k.adaptive_interval = p->adaptive_rho_interval;
+  k.polish_stable = p->polish_stable;
+  k.polish_refine = p->polish_refine;
+
+  hipError_t e = hipGetDevice(&pl->device);
+  if (e != hipSuccess) { delete pl; return hip_fail(e, "hipGetDevice"); }
+  int cus = 0;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pl->device);
+  if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
+  for (int q = 0; q < cmpc::kNumBins; ++q) {
+    int nb = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bin_fn(q), 64, 0);
+    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+    if (nb < 1) nb = 1;
+    pl->grid[q] = nb * cus;
+  }
+  e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
+  if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
+  e = hipMalloc(&pl->d_lists, (size_t)cmpc::kNumBins * p->max_batch * sizeof(int));
+  if (e != hipSuccess) {
+    (void)hipFree(pl->d_counters);
+    delete pl;
+    return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
+  }
+  *out = pl;
+  g_err.clear();
+  return CMPC_OK;
+}
+
+int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const float* gd,
+               const float* x0, const float* xref, const uint8_t* contact, float* w_out,
+               int32_t* status, int32_t* iters, void* stream) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_solve: null plan");
+  if (B < 0) return fail(CMPC_E_INVALID, "cmpc_solve: negative batch");
+  if (B == 0) return CMPC_OK;
+  if (B > pl->p.max_batch) return fail(CMPC_E_RANGE, "cmpc_solve: B exceeds plan max_batch");
+  if (!Ad || !Bd || !gd || !x0 || !xref || !contact || !w_out || !status || !iters)
+    return fail(CMPC_E_INVALID, "cmpc_solve: null array argument");
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t e = hipMemsetAsync(pl->d_counters, 0, 2 * cmpc::kNumBins * sizeof(int), st);
+  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  const int threads = 256;
+  const unsigned blocks = (unsigned)((B + threads - 1) / threads);
+  hipLaunchKernelGGL(cmpc::bin_kernel, dim3(blocks), dim3(threads), 0, st, pl->kp.N, B, contact,
+                     pl->d_counters, pl->d_lists, pl->p.max_batch);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
+  cmpc::Inputs in{Ad, Bd, gd, x0, xref, contact};
+  cmpc::Outputs out{w_out, status, iters};
+  for (int q = 0; q < cmpc::kNumBins; ++q) {
+    const int cap = cmpc::kBinCap[q];
+    if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) break;  // bins beyond 12N are empty
+    (void)cap;
+    const long long g = pl->grid[q] < B ? pl->grid[q] : B;
+    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(64), 0, st, pl->kp, in, out,
+                       pl->d_lists + (size_t)q * pl->p.max_batch, pl->d_counters + q,
+                       pl->d_counters + cmpc::kNumBins + q);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "solve_bin_kernel launch");
+  }
+  return CMPC_OK;
+}
+
+void cmpc_plan_destroy(cmpc_plan* pl) {
+  if (!pl) return;
+  (void)hipFree(pl->d_counters);
+  (void)hipFree(pl->d_lists);
+  delete pl;
+}
+
+const char* cmpc_last_error(void) { return g_err.c_str(); }
+
+const char* cmpc_version(void) { return "cmpc 1 gfx950"; }
+
+}  // extern "C"

@@ -1,0 +1,107 @@
+/*
+ * cmpc.h -- C-ABI of the MI355X batched convex-MPC contact-force QP solver.
+ *
+ * Drop-in boundary for the QP solve of ltinphan/convex-mpc-unitree-go2:
+ *   convex_mpc/centroidal_mpc.py:212-213  ca.conic('S', 'osqp', {h, a}, OPTS)   -> cmpc_plan_create
+ *   convex_mpc/centroidal_mpc.py:76-98    _update_sparse_matrix + _compute_bounds
+ *                                         + self.solver(h, g, a, lba, uba, lbx, ubx)
+ *                                                                                -> cmpc_solve
+ *   convex_mpc/centroidal_mpc.py:113-119  self.solver.stats()['return_status']  -> status[]
+ *
+ * One call solves B independent instances of the reference QP (centroidal_mpc.py:122-359):
+ *   min  sum_k (x_{k+1}-xref_k)' Q (x_{k+1}-xref_k) + u_k' R u_k
+ *   s.t. x_{k+1} = Ad x_k + Bd_k u_k + gd           (k = 0..N-1, x_0 given)
+ *        swing leg:  f = 0                           (centroidal_mpc.py:150-161)
+ *        stance leg: fz >= fz_min, |fx| <= mu fz, |fy| <= mu fz
+ *                                                    (centroidal_mpc.py:163-170, 264-283, 324-359)
+ * which is exactly ½w'Hw + g'w of the reference with H = diag(2Q.., 2R..), g = [-2Q xref; 0]
+ * (up to the constant sum xref'Q xref).
+ *
+ * Layouts (row-major, all device pointers, caller-owned):
+ *   Ad      [B][12][12]        fp32   (traj.Ad)
+ *   Bd      [B][N][12][12]     fp32   (traj.Bd)
+ *   gd      [B][12]            fp32   (traj.gd)
+ *   x0      [B][12]            fp32   (traj.initial_x_vec)
+ *   xref    [B][N][12]         fp32   (traj.compute_x_ref_vec() transposed: xref[b][k] is the
+ *                                      reference's column k = target for x_{k+1})
+ *   contact [B][4][N]          uint8  (traj.contact_table, legs FL FR RL RR; nonzero = stance)
+ *   w_out   [B][24N]           fp32   reference decision layout (centroidal_mpc.py:44,
+ *                                      test_MPC.py:190-192): w = [x_1..x_N | u_0..u_{N-1}],
+ *                                      each 12 contiguous, i.e. vec(X (12,N),'F') then vec(U,'F')
+ *   status  [B]                int32  1 solved (KKT-verified active-set polish),
+ *                                     2 solved inaccurate (ADMM residuals within eps, polish not
+ *                                       verified), -2 max iterations, -10 numerical failure
+ *   iters   [B]                int32  ADMM iterations taken
+ *
+ * Threading: one plan per host thread / stream.  cmpc_solve is asynchronous on `stream`
+ * (a hipStream_t, NULL = default stream); it performs no allocation, no host synchronisation
+ * and is graph-capturable.  Return codes are 0 or a negative CMPC_E* value; the message is
+ * available from cmpc_last_error() (thread-local).
+ */
+#ifndef CMPC_H_
+#define CMPC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMPC_ABI_VERSION 1
+
+#define CMPC_OK 0
+#define CMPC_E_INVALID (-22)   /* bad argument / parameter (EINVAL) */
+#define CMPC_E_NOMEM (-12)     /* device allocation failed (ENOMEM) */
+#define CMPC_E_HIP (-5)        /* HIP runtime error (EIO) */
+#define CMPC_E_RANGE (-34)     /* batch larger than the plan's max_batch (ERANGE) */
+
+/* Solver parameters.  cmpc_params_default() fills the reference's values
+ * (centroidal_mpc.py:12-38, fz_min from :127) and this solver's ADMM settings. */
+typedef struct cmpc_params {
+  int32_t abi_version;    /* must be CMPC_ABI_VERSION */
+  int32_t N;              /* horizon, 1..16 (reference: 16, com_trajectory.py:66) */
+  float Q[12];            /* state weight diagonal (centroidal_mpc.py:12) */
+  float R[12];            /* input weight diagonal (centroidal_mpc.py:13) */
+  float mu;               /* friction coefficient (centroidal_mpc.py:15) */
+  float fz_min;           /* stance normal-force lower bound (centroidal_mpc.py:127) */
+  float eps_abs;          /* ADMM residual tolerances for status 2 (OPTS eps_abs/eps_rel) */
+  float eps_rel;
+  int32_t max_iter;       /* ADMM iteration cap (OPTS max_iter) */
+  float rho;              /* initial ADMM penalty */
+  float sigma;            /* ADMM proximal regularisation (OSQP sigma) */
+  float alpha;            /* over-relaxation (OSQP alpha) */
+  int32_t adaptive_rho_interval; /* iterations between rho updates (0 = off) */
+  int32_t polish_stable;  /* polish after the active set is unchanged this many iterations */
+  int32_t polish_refine;  /* iterative-refinement steps inside the polish */
+  float polish_tol;       /* relative KKT tolerance for accepting the polished point */
+  int64_t max_batch;      /* largest B passed to cmpc_solve (sizes plan workspace) */
+} cmpc_params;
+
+typedef struct cmpc_plan cmpc_plan;
+
+/* Fill *p with defaults.  Replaces the OPTS dict (centroidal_mpc.py:20-36). */
+void cmpc_params_default(cmpc_params* p);
+
+/* Validate params, allocate workspace for max_batch instances on the current device.
+ * Replaces CentroidalMPC.__init__/_build_sparse_matrix (centroidal_mpc.py:41-67,178-230). */
+int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out);
+
+/* Solve B instances (see layouts above).  Replaces CentroidalMPC.solve_QP's update + solve
+ * (centroidal_mpc.py:69-120) for a whole batch.  `stream` is a hipStream_t or NULL. */
+int cmpc_solve(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd, const float* gd,
+               const float* x0, const float* xref, const uint8_t* contact, float* w_out,
+               int32_t* status, int32_t* iters, void* stream);
+
+void cmpc_plan_destroy(cmpc_plan* plan);
+
+/* Thread-local description of the last error returned on this thread ("" if none). */
+const char* cmpc_last_error(void);
+
+/* Build / ABI identification, e.g. "cmpc 1 gfx950". */
+const char* cmpc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CMPC_H_ */
