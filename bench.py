@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""bench.py -- batched convex-MPC QP solves/sec on MI355X (BASELINE.json metric).
+
+One *step* = one cmpc_solve over a resident batch of synthetic Go2 QP instances
+(default workload: config 1 distribution -- trot 3 Hz / duty 0.6 fixed
+contact schedule, seed 1 -- at ``--batch`` instances per GPU).  Instances are independent, so
+ranks shard them with no data-path collective (weak scaling: every rank solves its own
+``--batch`` instances, generated rank-locally from seed + rank); only the barrier and the
+max-over-ranks timing reduction use the process group.
+
+    python bench.py [--gpus N --steps K --warmup W --config 1|2|3 --batch B]
+
+Rank 0 prints one JSON line.  ``roofline`` prices the dominant solve kernel (the free-variable
+bin that holds most instances) against HBM: algorithmic bytes = 12,264 B per solve (inputs
+10,720 + outputs 1,544) x solves in that launch / its average HIP-event duration.
+``cpu_baseline`` times the oracle's C restatement of the reference's OSQP path
+(oracle/osqp_ref.c, float64, the reference's OPTS) on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
+
+BYTES_IN = 576 + 9216 + 48 + 48 + 768 + 64      # Ad, Bd, gd, x0, xref, contact (N=16, fp32/u8)
+BYTES_OUT = 1536 + 4 + 4                         # w, status, iters
+BYTES_PER_SOLVE = BYTES_IN + BYTES_OUT           # 12,264
+HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 3))
+    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--traffic-json", type=str, default=None,
+                    help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
+    ap.add_argument("--latency-batch", type=int, default=256)
+    return ap.parse_args()
+
+
+def bins_of(contact):
+    nf = 3 * (contact != 0).reshape(contact.shape[0], -1).sum(1)
+    caps = np.array([96, 128, 160, 192])
+    return np.searchsorted(caps, nf)   # first cap >= nf
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    from cmpc import Plan, SolverParams, to_device_batch, synth
+
+    B = args.batch
+    cfg = args.config
+    if cfg == 3:
+        batch = synth.make_config(3, B=B)
+    else:
+        batch = synth.make_batch(B, seed=synth.CONFIGS[cfg]["seed"] + 1000 * rank,
+                                 mixed=synth.CONFIGS[cfg]["mixed"])
+    bins = bins_of(batch["contact"])
+    d = to_device_batch(batch, dev)
+    plan = Plan(SolverParams(max_batch=B), device=dev)
+    w = torch.empty((B, 24 * 16), dtype=torch.float32, device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+    it = torch.empty((B,), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"],
+                   out=(w, st, it), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    plan.timing_read()
+    plan.set_timing(True)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    plan.set_timing(False)
+    ms_bins, calls = plan.timing_read()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    status = st.cpu().numpy()
+    iters = it.cpu().numpy()
+    solved_frac = float(np.mean(status == 1))
+    total = B * world * args.steps
+    value = total / elapsed
+
+    # dominant kernel: the bin with the most kernel time
+    q = int(np.argmax(ms_bins))
+    n_in_bin = int(np.sum(bins == q))
+    avg_ms = ms_bins[q] / max(calls[q], 1)
+    achieved_gbs = BYTES_PER_SOLVE * n_in_bin / (avg_ms * 1e-3) / 1e9
+    traffic = None
+    if args.traffic_json and Path(args.traffic_json).exists():
+        tj = json.loads(Path(args.traffic_json).read_text())
+        traffic = tj.get("hbm_bytes_per_launch")
+
+    # latency of one small batch (configs[1]: B=256) on the same plan
+    lb = min(args.latency_batch, B)
+    sl = {k: v[:lb] for k, v in d.items()}
+    for _ in range(3):
+        plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
+    torch.cuda.synchronize(dev)
+    tl0 = time.perf_counter()
+    for _ in range(10):
+        plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
+    torch.cuda.synchronize(dev)
+    lat_ms = (time.perf_counter() - tl0) / 10 * 1e3
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(batch, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "batched QP solves/sec (N=16, 4-leg friction cone) at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": f"cfg{cfg} Go2 QP batch (SURVEY.md 8(d)), "
+                                   f"{'trot 3Hz/0.6 fixed schedule' if cfg == 1 else 'mixed stance' if cfg == 2 else 'trot+mixed'}",
+                       "N": 16, "batch_per_gpu": B, "global_batch": B * world,
+                       "parallelism": f"instance-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "kernel": f"solve_bin_kernel<{[96, 128, 160, 192][q]}>",
+                         "kernel_avg_ms": avg_ms, "solves_per_launch": n_in_bin,
+                         "bytes_per_solve": BYTES_PER_SOLVE},
+            "cpu_baseline": cpu,
+            "solved_frac": solved_frac,
+            "iters_mean": float(np.mean(iters)),
+            "latency_ms_b256": lat_ms,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(batch, seconds):
+    """Time oracle/osqp_ref (C restatement of the reference's OSQP solve) on host cores."""
+    try:
+        sys.path.insert(0, str(REPO))
+        from oracle import osqp_ref
+    except Exception as e:  # pragma: no cover - reported, not fatal
+        return {"value": None, "unit": "solves/s", "cores": 0, "kind": "port",
+                "sample": f"unavailable: {e}"}
+    return osqp_ref.time_baseline(batch, seconds)
+
+
+if __name__ == "__main__":
+    main()

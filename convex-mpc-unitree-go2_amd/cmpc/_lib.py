@@ -38,7 +38,9 @@ class CParams(ctypes.Structure):
 
 
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
-           "cmpc_last_error", "cmpc_version")
+           "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_last_error", "cmpc_version")
+NUM_BINS = 4
+BIN_CAPS = (96, 128, 160, 192)
 
 _lib = None
 
@@ -62,6 +64,11 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
     lib.cmpc_solve.restype = ctypes.c_int
     lib.cmpc_plan_destroy.argtypes = [vp]
     lib.cmpc_plan_destroy.restype = None
+    lib.cmpc_plan_set_timing.argtypes = [vp, ctypes.c_int]
+    lib.cmpc_plan_set_timing.restype = ctypes.c_int
+    lib.cmpc_plan_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_float),
+                                          ctypes.POINTER(ctypes.c_int32)]
+    lib.cmpc_plan_timing_read.restype = ctypes.c_int
     lib.cmpc_last_error.argtypes = []
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_version.argtypes = []

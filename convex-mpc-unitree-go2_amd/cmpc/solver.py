@@ -105,6 +105,18 @@ class Plan:
         except Exception:
             pass
 
+    def set_timing(self, enable: bool):
+        _check(self.lib, self.lib.cmpc_plan_set_timing(self._h, int(bool(enable))),
+               "cmpc_plan_set_timing")
+
+    def timing_read(self):
+        """-> (ms_per_bin[4], calls_per_bin[4]) of the solve kernels since the last read."""
+        ms = (ctypes.c_float * _lib.NUM_BINS)()
+        calls = (ctypes.c_int32 * _lib.NUM_BINS)()
+        _check(self.lib, self.lib.cmpc_plan_timing_read(self._h, ms, calls),
+               "cmpc_plan_timing_read")
+        return list(ms), list(calls)
+
     def solve(self, Ad, Bd, gd, x0, xref, contact, out=None, stream=None):
         """Solve B instances; all inputs are device tensors (layouts: include/cmpc.h).
 

@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <string>
+#include <vector>
 
 #include "cmpc.h"
 #include "cmpc_device.h"
@@ -18,7 +19,14 @@ struct cmpc_plan {
   int device;
   int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
+  float* d_work;    // per-workgroup staging + park slabs (largest bin's need)
   int grid[cmpc::kNumBins];
+  int threads[cmpc::kNumBins];
+  // timing hooks
+  bool timing = false;
+  struct Rec { hipEvent_t a, b; int bin; };
+  std::vector<Rec> recs;       // recorded (pending) pairs
+  std::vector<Rec> pool;       // free event pairs
 };
 
 namespace {
@@ -34,7 +42,25 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 using KernelFn = void (*)(cmpc::KParams, cmpc::Inputs, cmpc::Outputs, const int*, const int*,
-                          int*);
+                          int*, float*);
+
+int bin_threads(int q) {
+  switch (q) {
+    case 0: return cmpc::Cfg<96>::THREADS;
+    case 1: return cmpc::Cfg<128>::THREADS;
+    case 2: return cmpc::Cfg<160>::THREADS;
+    default: return cmpc::Cfg<192>::THREADS;
+  }
+}
+
+size_t bin_slab(int q) {
+  switch (q) {
+    case 0: return cmpc::Cfg<96>::SLAB;
+    case 1: return cmpc::Cfg<128>::SLAB;
+    case 2: return cmpc::Cfg<160>::SLAB;
+    default: return cmpc::Cfg<192>::SLAB;
+  }
+}
 
 KernelFn bin_fn(int q) {
   switch (q) {
@@ -121,18 +147,29 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   int cus = 0;
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pl->device);
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
+  size_t work_floats = 0;
   for (int q = 0; q < cmpc::kNumBins; ++q) {
     int nb = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bin_fn(q), 64, 0);
+    pl->threads[q] = bin_threads(q);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bin_fn(q), pl->threads[q], 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
     pl->grid[q] = nb * cus;
+    const size_t need = (size_t)pl->grid[q] * 2 * bin_slab(q);
+    if (need > work_floats) work_floats = need;
   }
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
+  e = hipMalloc(&pl->d_work, work_floats * sizeof(float));
+  if (e != hipSuccess) {
+    (void)hipFree(pl->d_counters);
+    delete pl;
+    return fail(CMPC_E_NOMEM, "hipMalloc workspace failed");
+  }
   e = hipMalloc(&pl->d_lists, (size_t)cmpc::kNumBins * p->max_batch * sizeof(int));
   if (e != hipSuccess) {
     (void)hipFree(pl->d_counters);
+    (void)hipFree(pl->d_work);
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
@@ -166,21 +203,77 @@ int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const
     if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) break;  // bins beyond 12N are empty
     (void)cap;
     const long long g = pl->grid[q] < B ? pl->grid[q] : B;
-    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(64), 0, st, pl->kp, in, out,
-                       pl->d_lists + (size_t)q * pl->p.max_batch, pl->d_counters + q,
-                       pl->d_counters + cmpc::kNumBins + q);
+    cmpc_plan::Rec rec{nullptr, nullptr, q};
+    const bool rec_this = pl->timing && pl->recs.size() < 4096 * cmpc::kNumBins;
+    if (rec_this) {
+      if (!pl->pool.empty()) {
+        rec = pl->pool.back();
+        pl->pool.pop_back();
+        rec.bin = q;
+      } else {
+        if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+        if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+      }
+      if ((e = hipEventRecord(rec.a, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    }
+    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(pl->threads[q]), 0, st, pl->kp, in,
+                       out, pl->d_lists + (size_t)q * pl->p.max_batch, pl->d_counters + q,
+                       pl->d_counters + cmpc::kNumBins + q, pl->d_work);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "solve_bin_kernel launch");
+    if (rec_this) {
+      if ((e = hipEventRecord(rec.b, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+      pl->recs.push_back(rec);
+    }
   }
+  return CMPC_OK;
+}
+
+int cmpc_plan_set_timing(cmpc_plan* pl, int enable) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_timing: null plan");
+  pl->timing = enable != 0;
+  return CMPC_OK;
+}
+
+int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_bin, int32_t* calls_per_bin) {
+  if (!pl || !ms_per_bin || !calls_per_bin)
+    return fail(CMPC_E_INVALID, "cmpc_plan_timing_read: null argument");
+  for (int q = 0; q < cmpc::kNumBins; ++q) { ms_per_bin[q] = 0.f; calls_per_bin[q] = 0; }
+  for (auto& r : pl->recs) {
+    hipError_t e = hipEventSynchronize(r.b);
+    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+    float ms = 0.f;
+    e = hipEventElapsedTime(&ms, r.a, r.b);
+    if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+    ms_per_bin[r.bin] += ms;
+    calls_per_bin[r.bin] += 1;
+    pl->pool.push_back(r);
+  }
+  pl->recs.clear();
   return CMPC_OK;
 }
 
 void cmpc_plan_destroy(cmpc_plan* pl) {
   if (!pl) return;
+  for (auto& r : pl->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (auto& r : pl->pool) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   (void)hipFree(pl->d_counters);
   (void)hipFree(pl->d_lists);
+  (void)hipFree(pl->d_work);
   delete pl;
 }
+
+#ifdef CMPC_STAMPS
+// diagnostic build only: read and clear the per-phase cycle counters
+int cmpc_debug_stamps(unsigned long long* out16) {
+  hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(cmpc::g_stamps), 16 * sizeof(unsigned long long));
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyFromSymbol");
+  unsigned long long z[16] = {0};
+  e = hipMemcpyToSymbol(HIP_SYMBOL(cmpc::g_stamps), z, sizeof(z));
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyToSymbol");
+  return CMPC_OK;
+}
+#endif
 
 const char* cmpc_last_error(void) { return g_err.c_str(); }
 

@@ -94,6 +94,14 @@ int cmpc_solve(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd, con
 
 void cmpc_plan_destroy(cmpc_plan* plan);
 
+/* Measurement hooks (not on the reference's interface; used by bench.py).  While enabled,
+ * cmpc_solve records a hipEvent pair on `stream` around every solve-kernel launch (one per
+ * free-variable bin).  cmpc_plan_timing_read waits for the recorded events, returns the
+ * summed kernel milliseconds per bin (ms_per_bin[4]) and launch counts (calls_per_bin[4]) since
+ * the last read, and resets them.  At most 4096 solve calls are recorded between reads. */
+int cmpc_plan_set_timing(cmpc_plan* plan, int enable);
+int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_bin, int32_t* calls_per_bin);
+
 /* Thread-local description of the last error returned on this thread ("" if none). */
 const char* cmpc_last_error(void);
 

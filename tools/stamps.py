@@ -1,0 +1,48 @@
+"""Diagnostic: per-phase cycle shares of the solve kernel (libcmpc_stamps.so, -DCMPC_STAMPS).
+
+    python tools/stamps.py [--config 1] [--batch 8192]
+"""
+import argparse
+import ctypes
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=8192)
+    a = ap.parse_args()
+    import torch
+    from cmpc import _lib, synth
+    lib = _lib.load(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_stamps.so")
+    _lib._lib = lib
+    lib.cmpc_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    from cmpc import Plan, SolverParams, to_device_batch
+    b = synth.make_batch(a.batch, seed=1, mixed=(a.config == 2))
+    d = to_device_batch(b)
+    plan = Plan(SolverParams(max_batch=a.batch))
+    buf = (ctypes.c_ulonglong * 16)()
+    plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+    torch.cuda.synchronize()
+    lib.cmpc_debug_stamps(buf)
+    w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+    torch.cuda.synchronize()
+    lib.cmpc_debug_stamps(buf)
+    v = np.array(list(buf), dtype=np.float64)
+    n = v[10]
+    names = ["condense", "invert", "gradient", "symv", "polish(all)", "instance total"]
+    print(f"instances {int(n)}  mean iters {v[11]/n:.2f}  condense_invert/inst {v[8]/n:.2f}  "
+          f"polish attempts/inst {v[9]/n:.2f}")
+    for i, nm in enumerate(names):
+        print(f"  {nm:16s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
+    print("  status:", dict(zip(*np.unique(st.cpu().numpy(), return_counts=True))))
+
+
+if __name__ == "__main__":
+    main()
