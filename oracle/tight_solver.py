@@ -44,7 +44,8 @@ def _split_constraints(qp):
             G_rows.append(I[i]); h.append(hi); in_map.append(('x', i, 1.0))
         if np.isfinite(lo):
             G_rows.append(-I[i]); h.append(-lo); in_map.append(('x', i, -1.0))
-    return (np.array(E_rows), np.array(b), eq_map, np.array(G_rows), np.array(h), in_map)
+    return (np.array(E_rows).reshape(-1, n), np.array(b, dtype=float), eq_map,
+            np.array(G_rows).reshape(-1, n), np.array(h, dtype=float), in_map)
 
 
 def _to_casadi_duals(n, m, nu, lam, eq_map, in_map):
@@ -68,6 +69,15 @@ def solve(qp, tol: float = 1e-13, max_iter: int = 80, polish: bool = True):
     m = qp['a'].shape[0]
     E, b, eq_map, G, h, in_map = _split_constraints(qp)
     me, mi = E.shape[0], G.shape[0]
+    if mi == 0:  # equality-constrained only (e.g. every leg in swing): one KKT solve
+        K = np.zeros((n + me, n + me))
+        K[:n, :n] = H
+        K[:n, n:] = E.T
+        K[n:, :n] = E
+        sol = np.linalg.solve(K, np.concatenate([-g, b]))
+        lam_x, lam_a = _to_casadi_duals(n, m, sol[n:], np.zeros(0), eq_map, in_map)
+        return dict(w=sol[:n], lam_x=lam_x, lam_a=lam_a, iters=0,
+                    kkt=mpc_qp.kkt_residuals(qp, sol[:n], lam_x, lam_a), polished=True)
 
     w = np.zeros(n)
     nu = np.zeros(me)

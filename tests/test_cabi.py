@@ -1,0 +1,81 @@
+"""CPU: the C-ABI library loads, exports every symbol include/cmpc.h declares, and
+validates parameters without touching a GPU."""
+import ctypes
+import re
+
+import pytest
+
+from conftest import REPO
+
+
+def declared_symbols():
+    h = (REPO / "include" / "cmpc.h").read_text()
+    return sorted(set(re.findall(r"\b(cmpc_[a-z_]+)\s*\(", h)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from cmpc import _lib
+    from cmpc.build import build_library, LIB
+    if not LIB.exists():
+        build_library()
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    syms = declared_symbols()
+    assert len(syms) >= 8
+    for s in syms:
+        assert hasattr(lib, s), s
+    from cmpc import _lib
+    assert set(_lib.EXPORTS) <= set(syms)
+
+
+def test_defaults_are_reference_constants(lib):
+    from cmpc import _lib
+    p = _lib.CParams()
+    lib.cmpc_params_default(ctypes.byref(p))
+    assert p.abi_version == _lib.ABI_VERSION and p.N == 16
+    assert list(p.Q) == [1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1]        # centroidal_mpc.py:12
+    assert all(abs(r - 1e-5) < 1e-12 for r in p.R)                       # :13
+    assert abs(p.mu - 0.8) < 1e-7 and p.fz_min == 10.0                   # :15, :127
+    assert abs(p.eps_abs - 1e-4) < 1e-9 and p.max_iter == 1000           # :25-27
+    assert p.adaptive_rho_interval == 25                                 # :32
+    assert lib.cmpc_version().decode().startswith("cmpc 1")
+
+
+@pytest.mark.parametrize("field,value", [("N", 0), ("N", 17), ("mu", -1.0), ("max_iter", 0),
+                                         ("alpha", 2.5), ("rho", 0.0), ("max_batch", 0)])
+def test_invalid_params_rejected_before_device(lib, field, value):
+    from cmpc import _lib
+    p = _lib.CParams()
+    lib.cmpc_params_default(ctypes.byref(p))
+    setattr(p, field, value)
+    h = ctypes.c_void_p()
+    rc = lib.cmpc_plan_create(ctypes.byref(p), ctypes.byref(h))
+    assert rc == -22
+    assert "cmpc_plan_create" in lib.cmpc_last_error().decode()
+
+
+def test_null_arguments(lib):
+    assert lib.cmpc_plan_create(None, None) == -22
+    assert lib.cmpc_solve(None, 1, *([None] * 10)) == -22
+    assert lib.cmpc_plan_set_timing(None, 1) == -22
+    lib.cmpc_plan_destroy(None)
+
+
+def test_python_params_roundtrip():
+    from cmpc import SolverParams
+    c = SolverParams(N=12, mu=0.6, max_batch=7).to_c()
+    assert c.N == 12 and abs(c.mu - 0.6) < 1e-7 and c.max_batch == 7
+    with pytest.raises(ValueError):
+        SolverParams(Q=(1, 2)).to_c()
+
+
+def test_no_cpu_fallback_without_device():
+    import torch
+    from cmpc import Plan, CmpcError
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    with pytest.raises(CmpcError):
+        Plan()

@@ -1,0 +1,102 @@
+"""CPU: the oracle (oracle/) against the reference's own outputs and invariants.
+
+ref_inputs.npz was produced by running the reference's gait.py / com_trajectory.py
+(tests/golden/make_golden.py); the QP fixtures hold KKT-certified optima.
+"""
+import numpy as np
+import pytest
+
+from oracle import mpc_qp, tight_solver
+from cmpc import synth
+from parity_util import load_fixture, fixture_batch
+
+
+def _cases():
+    z = load_fixture("ref_inputs.npz")
+    n = int(z["n_cases"])
+    return [{k[len(f"c{i}_"):]: v for k, v in z.items() if k.startswith(f"c{i}_")} for i in range(n)]
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: f"hz{c['hz']}_duty{c['duty']}")
+def test_contact_table_matches_reference(case):
+    N = int(case["N"])
+    ct = mpc_qp.contact_table(float(case["t_now"]), float(case["dt"]), N, float(case["hz"]),
+                              float(case["duty"]))
+    assert np.array_equal(ct, case["contact"])
+    ct2 = synth.contact_table(float(case["t_now"]), float(case["dt"]), N, float(case["hz"]),
+                              float(case["duty"]))
+    assert np.array_equal(ct2.astype(np.int32), case["contact"])
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: f"hz{c['hz']}_duty{c['duty']}")
+def test_dynamics_match_reference(case):
+    r_legs = case["r_legs"]                       # (N, 4, 3)
+    Ac, Bc, gc = mpc_qp.continuous_dynamics(float(case["m"]), case["I"], r_legs,
+                                            float(case["yaw_avg"]))
+    assert np.allclose(Ac, case["Ac"], atol=1e-14)
+    assert np.allclose(Bc, case["Bc"], atol=1e-12)
+    assert np.allclose(gc, case["gc"])
+    Ad, Bd, gd = mpc_qp.discrete_dynamics(Ac, Bc, gc, float(case["dt"]))
+    assert np.allclose(Ad, case["Ad"], atol=1e-13)
+    assert np.allclose(Bd, case["Bd"], atol=1e-13)
+    assert np.allclose(gd, case["gd"], atol=1e-13)
+    Ad2, Bd2, gd2 = mpc_qp.discrete_dynamics_closed_form(Ac, Bc, gc, float(case["dt"]))
+    assert np.allclose(Ad2, case["Ad"], atol=1e-13)
+    assert np.allclose(Bd2, case["Bd"], atol=1e-13)
+    assert np.allclose(gd2, case["gd"], atol=1e-13)
+    # the product-side batched generator uses the same closed form
+    Ad3, Bd3, gd3 = synth.discretize(np.array([case["m"]]), case["I"][None], r_legs[None],
+                                     np.array([case["yaw_avg"]]), float(case["dt"]))
+    assert np.allclose(Ad3[0], case["Ad"], atol=1e-13)
+    assert np.allclose(Bd3[0], case["Bd"], atol=1e-13)
+    assert np.allclose(gd3[0], case["gd"], atol=1e-13)
+
+
+def test_qp_structure_matches_reference_print():
+    """centroidal_mpc.py:225-230 invariants: H 384x384 nnz 384; A 448x384 nnz 5168 (0.0300)."""
+    b = synth.make_config(1, B=1)
+    qp = mpc_qp.build_qp(b["Ad"][0], b["Bd"][0], b["gd"][0], b["x0"][0], b["xref"][0].T,
+                         b["contact"][0])
+    assert qp["h"].shape == (384, 384) and qp["h"].nnz == 384
+    assert qp["a"].shape == (448, 384) and qp["a"].nnz == 5168 == mpc_qp.structural_nnz(16)
+    assert round(5168 / (448 * 384), 4) == 0.0300
+    assert qp["lba"].shape == (448,) and qp["lbx"].shape == (384,)
+
+
+@pytest.mark.parametrize("name", ["qp_cfg1.npz", "qp_cfg2.npz"])
+def test_golden_fixtures_are_kkt_certified(name):
+    fx = load_fixture(name)
+    for i in range(0, fx["w"].shape[0], 8):
+        qp = mpc_qp.build_qp(fx["Ad"][i], fx["Bd"][i], fx["gd"][i], fx["x0"][i], fx["xref"][i].T,
+                             fx["contact"][i])
+        k = mpc_qp.kkt_residuals(qp, fx["w"][i], fx["lam_x"][i], fx["lam_a"][i])
+        assert max(k.values()) < 1e-8, (i, k)
+
+
+def test_tight_solver_certifies_fresh_instance():
+    b = synth.make_config(2, B=3)
+    qp = mpc_qp.build_qp(b["Ad"][2], b["Bd"][2], b["gd"][2], b["x0"][2], b["xref"][2].T,
+                         b["contact"][2])
+    r = tight_solver.solve(qp)
+    assert max(r["kkt"].values()) < 1e-8
+
+
+def test_rollout_matches_equality_rows():
+    fx = load_fixture("qp_cfg1.npz")
+    X, U = mpc_qp.unpack_w(fx["w"][0])
+    Xr = mpc_qp.rollout(fx["Ad"][0], fx["Bd"][0], fx["gd"][0], fx["x0"][0], U.T)
+    assert np.allclose(Xr.T, X, atol=1e-9)
+
+
+def test_duals_recovered_from_primal():
+    """cmpc.duals (host post-processing of the single-robot API) reproduces the certified
+    multipliers from the certified primal."""
+    from cmpc import duals
+    fx = load_fixture("qp_cfg2.npz")
+    for i in range(4):
+        lx, la = duals.recover(fx["Ad"][i], fx["Bd"][i], fx["gd"][i], fx["x0"][i], fx["xref"][i],
+                               fx["contact"][i], fx["w"][i], mpc_qp.Q_DIAG, mpc_qp.R_DIAG,
+                               mpc_qp.MU, mpc_qp.FZ_MIN)
+        scale = max(1e-3, np.max(np.abs(fx["lam_a"][i])))
+        assert np.max(np.abs(la - fx["lam_a"][i])) < 1e-6 * scale + 1e-9
+        assert np.max(np.abs(lx - fx["lam_x"][i])) < 1e-6 * scale + 1e-9
