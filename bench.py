@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=65536, help="instances per GPU per step")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--traffic-json", type=str, default=None,
+    ap.add_argument("--traffic-json", type=str, default=str(REPO / "profiles" / "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
     ap.add_argument("--latency-batch", type=int, default=256)
     return ap.parse_args()

@@ -33,6 +33,7 @@ class CParams(ctypes.Structure):
         ("polish_stable", ctypes.c_int32),
         ("polish_refine", ctypes.c_int32),
         ("polish_tol", ctypes.c_float),
+        ("polish_repairs", ctypes.c_int32),
         ("max_batch", ctypes.c_int64),
     ]
 

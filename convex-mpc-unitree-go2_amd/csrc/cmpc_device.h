@@ -18,6 +18,7 @@ struct KParams {
   int adaptive_interval;
   int polish_stable;
   int polish_refine;
+  int polish_repairs;
 };
 
 // Device pointers of one cmpc_solve call (layouts: include/cmpc.h).

@@ -19,7 +19,7 @@ struct cmpc_plan {
   int device;
   int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
-  float* d_work;    // per-workgroup staging + park slabs (largest bin's need)
+  float* d_work;    // per-workgroup park slabs (largest bin's need)
   int grid[cmpc::kNumBins];
   int threads[cmpc::kNumBins];
   // timing hooks
@@ -96,6 +96,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_stable = 3;
   p->polish_refine = 4;
   p->polish_tol = 1e-5f;
+  p->polish_repairs = 3;
   p->max_batch = 65536;
 }
 
@@ -116,7 +117,8 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (p->max_iter < 1) return fail(CMPC_E_INVALID, "cmpc_plan_create: max_iter must be >= 1");
   if (!(p->rho > 0.f) || !(p->sigma >= 0.f) || !(p->alpha > 0.f && p->alpha < 2.f))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: need rho > 0, sigma >= 0, 0 < alpha < 2");
-  if (p->polish_stable < 1 || p->polish_refine < 1 || !(p->polish_tol > 0.f))
+  if (p->polish_stable < 1 || p->polish_refine < 1 || !(p->polish_tol > 0.f) ||
+      p->polish_repairs < 0)
     return fail(CMPC_E_INVALID, "cmpc_plan_create: polish settings out of range");
   if (p->adaptive_rho_interval < 0 || p->max_batch < 1 || p->max_batch > (1LL << 30))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: adaptive_rho_interval/max_batch out of range");
@@ -141,6 +143,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   k.adaptive_interval = p->adaptive_rho_interval;
   k.polish_stable = p->polish_stable;
   k.polish_refine = p->polish_refine;
+  k.polish_repairs = p->polish_repairs;
 
   hipError_t e = hipGetDevice(&pl->device);
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipGetDevice"); }
@@ -155,7 +158,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
     pl->grid[q] = nb * cus;
-    const size_t need = (size_t)pl->grid[q] * 2 * bin_slab(q);
+    const size_t need = (size_t)pl->grid[q] * bin_slab(q);
     if (need > work_floats) work_floats = need;
   }
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));

@@ -9,7 +9,7 @@
 //      W_ij = A'W_{i+1,j}, H_ij = B_i'W_ij.  Every 12x12 product is a chain of four
 //      v_mfma_f32_16x16x4_f32 (12 padded to 16) whose accumulator feeds the next MFMA as its
 //      B operand without leaving registers (k is permuted as k = 4*(lane>>4) + step).  The
-//      waves of the workgroup split the j loop; H goes to a per-workgroup staging slab.
+//      waves of the workgroup split the j loop; H is staged in LDS in tile layout.
 //   2. The symmetric H + diag(R) + shift is held in REGISTERS as 8x8 tiles of its lower
 //      triangle, one tile per lane (workgroup = ceil(tiles/64) waves), and inverted in place
 //      by the symmetric sweep operator (Gauss-Jordan on the unit-diagonal-scaled matrix):
@@ -22,8 +22,8 @@
 //      accurate as that gradient, not eps32 x cond(H).
 //   4. Active-set polish once the face pattern of z is stable: condense + invert the
 //      equality-constrained reduced problem (u = T v + t0), refine with the accurate gradient,
-//      accept only if the KKT conditions hold -> status 1.  The ADMM inverse is parked in the
-//      workgroup's global slab during the attempt and restored if it fails.
+//      accept only if the KKT conditions hold -> status 1.  The ADMM inverse is parked in a
+//      per-workgroup global slab (L2-resident) during the attempt and restored if it fails.
 //
 // Instances are binned by free-variable count (capacity NC in {96,128,160,192}); each bin
 // runs a persistent kernel pulling instance ids from a device-side queue.
@@ -101,7 +101,9 @@ struct Cfg {
   static constexpr int NT = TT * (TT + 1) / 2;           // lower-triangle tiles
   static constexpr int THREADS = ((NT + 63) / 64) * 64;  // one tile per lane
   static constexpr int WAVES = THREADS / 64;
-  static constexpr int SLAB = NT * 64;                   // floats per staging / park slab
+  static constexpr int SLAB = NT * 64;                   // floats per park slab (global)
+  static constexpr int TS = 68;                          // LDS staging tile stride (floats):
+  // a lane reading its own tile then hits bank (4t + c) mod 64 -> conflict-free 16-B reads
 };
 
 template <int NC>
@@ -120,6 +122,7 @@ struct Smem {
   alignas(16) float av[2][NC];     // sweep pivot column (double buffered)
   alignas(16) float ds[NC];        // unit-diagonal scaling
   alignas(16) float part[Cfg<NC>::NT * 16];  // symv partial sums per tile (rows | cols)
+  alignas(16) float stg[Cfg<NC>::NT * Cfg<NC>::TS];  // condensation output, tile layout
   float D[kMaxP];                  // d_k  (error-coordinate affine term)
   float Dt[kMaxP];                 // d~_k (d_k + B_k t0_k in the polish basis)
   float H[kMaxP];                  // h_k = B~_k v_k + d~_k
@@ -164,15 +167,16 @@ __device__ __forceinline__ f4 load_bcol(const Smem<NC>& s, int p0, int m, int g,
   return v;
 }
 
-__device__ __forceinline__ void stage_store(float* __restrict__ stg, int p, int q, float val) {
+template <int TS>
+__device__ __forceinline__ void stage_store(float* stg, int p, int q, float val) {
   // p >= q; diagonal tiles keep both halves
   const int t = tile_index(p >> 3, q >> 3);
-  stg[t * 64 + (p & 7) * 8 + (q & 7)] = val;
-  if ((p >> 3) == (q >> 3) && p != q) stg[t * 64 + (q & 7) * 8 + (p & 7)] = val;
+  stg[t * TS + (p & 7) * 8 + (q & 7)] = val;
+  if ((p >> 3) == (q >> 3) && p != q) stg[t * TS + (q & 7) * 8 + (p & 7)] = val;
 }
 
 template <int NC>
-__device__ __forceinline__ void condense_stage(const Smem<NC>& s, const KParams& P, float* __restrict__ stg) {
+__device__ __forceinline__ void condense_stage(Smem<NC>& s, const KParams& P) {
   using C = Cfg<NC>;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
@@ -234,23 +238,23 @@ __device__ __forceinline__ void condense_stage(const Smem<NC>& s, const KParams&
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int qq = 4 * g + q;
-        if (qq < mi && c < mj && (i != j || c >= qq)) stage_store(stg, pj0 + c, pi0 + qq, Hb[q]);
+        if (qq < mi && c < mj && (i != j || c >= qq))
+          stage_store<C::TS>(s.stg, pj0 + c, pi0 + qq, Hb[q]);
       }
     }
   }
 }
 
-// register tile <- staging slab, + diag(Rt) + shift, identity on padding
+// register tile <- LDS staging, + diag(Rt) + shift, identity on padding
 template <int NC>
-__device__ __forceinline__ void load_tile(float (&T)[64], const float* __restrict__ stg,
-                                          const Smem<NC>& s, int I, int J, bool own, int n,
-                                          float shift) {
+__device__ __forceinline__ void load_tile(float (&T)[64], const Smem<NC>& s, int I, int J,
+                                          bool own, int n, float shift) {
   if (!own) {
 #pragma unroll
     for (int q = 0; q < 64; ++q) T[q] = 0.f;
     return;
   }
-  const f4* src = reinterpret_cast<const f4*>(stg + tile_index(I, J) * 64);
+  const f4* src = reinterpret_cast<const f4*>(&s.stg[tile_index(I, J) * Cfg<NC>::TS]);
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const f4 v = src[q];
@@ -629,16 +633,20 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P, cons
     const float tol_d = P.polish_tol * gs, tol_p = P.polish_tol * us;
     bool ok = true;
     if (tf.owns) {
+      // KKT per triple; on a violation also derive the repaired face set (primal-dual
+      // active-set step): drop faces with a negative multiplier, add violated faces
       const float lx = sx ? -sx * gx : 0.f;
       const float ly = sy ? -sy * gy : 0.f;
       const float l0 = gz - mu * (lx + ly);
-      if (sx && lx < -tol_d) ok = false;
-      if (sy && ly < -tol_d) ok = false;
-      if (tf.zl && l0 < -tol_d) ok = false;
-      if (!sx && fabsf(fx) > mu * fz + tol_p) ok = false;
-      if (!sy && fabsf(fy) > mu * fz + tol_p) ok = false;
-      if (!tf.zl && fz < fzmin - tol_p) ok = false;
+      int nc = s.code[tid];
+      if (sx && lx < -tol_d) { ok = false; nc &= ~6; }
+      if (sy && ly < -tol_d) { ok = false; nc &= ~24; }
+      if (tf.zl && l0 < -tol_d) { ok = false; nc &= ~1; }
+      if (!sx && fabsf(fx) > mu * fz + tol_p) { ok = false; nc |= (fx > 0.f) ? 2 : 4; }
+      if (!sy && fabsf(fy) > mu * fz + tol_p) { ok = false; nc |= (fy > 0.f) ? 8 : 16; }
+      if (!tf.zl && fz < fzmin - tol_p) { ok = false; nc |= 1; }
       if (!(isfinite(fx) && isfinite(fy) && isfinite(fz))) ok = false;
+      s.tcnt[tid] = nc;  // repaired code (copied into s.code by the caller if used)
     }
     const bool all_ok = (__all(ok) != 0) && (step <= P.polish_tol * us);
     if (all_ok && tf.owns) {
@@ -646,7 +654,12 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P, cons
       s.U[12 * k + 3 * leg + 1] = fy;
       s.U[12 * k + 3 * leg + 2] = fz;
     }
-    if (tid == 0) s.ctl[2] = all_ok ? 1 : 0;
+    const bool changed = tf.owns && (s.tcnt[tid] != s.code[tid]);
+    const bool any_changed = __any(changed) != 0;
+    if (tid == 0) {
+      s.ctl[2] = all_ok ? 1 : 0;
+      s.ctl[4] = any_changed ? 1 : 0;
+    }
   }
   __syncthreads();
   return s.ctl[2] != 0;
@@ -657,7 +670,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P, cons
 template <int NC>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
-                                               float* __restrict__ stg, float* __restrict__ park,
+                                               float* __restrict__ park,
                                                float (&T)[64], int I, int J, bool own) {
   using C = Cfg<NC>;
   const int tid = threadIdx.x;
@@ -707,6 +720,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   float shift = P.sigma + rho;
   TripleFaces tf;
   int it = 0;
+  int repairs_left = 0;
+  float nq = 0.f;                  // |q| of the condensed QP (= |grad f(0)|, iteration 1)
   const float alpha = P.alpha;
   if (n == 0) status = 1;
   while (n > 0) {
@@ -714,9 +729,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       CMPC_CNT(8, 1);
       CMPC_T0(t_c);
       __syncthreads();
-      condense_stage<NC>(s, P, stg);
+      condense_stage<NC>(s, P);
       __syncthreads();
-      load_tile<NC>(T, stg, s, I, J, own, nact, shift);
+      load_tile<NC>(T, s, I, J, own, nact, shift);
       CMPC_ACC(0, t_c);
       CMPC_T0(t_i);
       invert_tile<NC>(s, T, I, J, own, nact);
@@ -743,6 +758,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         polished = true;
         status = 1;
         break;
+      }
+      if (repairs_left > 0 && s.ctl[4]) {  // re-polish on the repaired face set
+        --repairs_left;
+        for (int t = tid; t < ntri; t += C::THREADS) s.code[t] = s.tcnt[t];
+        nact = polish_setup<NC>(s, P, Bg, ntri, tf);
+        shift = P.sigma;
+        refactor = true;
+        continue;
       }
       // restore the parked ADMM inverse and basis, continue ADMM
       if (own) {
@@ -843,6 +866,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       shift = P.sigma;
       refactor = true;
       in_polish = true;
+      repairs_left = P.polish_repairs;
     }
   }
   if (n > 0 && !polished) {
@@ -891,8 +915,7 @@ __global__ void __launch_bounds__(Cfg<NC>::THREADS, 2)
   while ((I + 1) * (I + 2) / 2 <= tid) ++I;
   const int J = tid - I * (I + 1) / 2;
   if (!own) I = 1 << 20;
-  float* stg = work + (size_t)blockIdx.x * 2 * C::SLAB;
-  float* park = stg + C::SLAB;
+  float* park = work + (size_t)blockIdx.x * C::SLAB;
   float T[64];
 #pragma unroll
   for (int q = 0; q < 64; ++q) T[q] = 0.f;
@@ -907,7 +930,7 @@ __global__ void __launch_bounds__(Cfg<NC>::THREADS, 2)
     const int idx = s.ctl[7];
     __syncthreads();
     if (idx >= total) break;
-    solve_instance<NC>(s, P, (int64_t)list[idx], in, out, stg, park, T, I, J, own);
+    solve_instance<NC>(s, P, (int64_t)list[idx], in, out, park, T, I, J, own);
   }
 }
 

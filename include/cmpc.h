@@ -74,6 +74,8 @@ typedef struct cmpc_params {
   int32_t polish_stable;  /* polish after the active set is unchanged this many iterations */
   int32_t polish_refine;  /* iterative-refinement steps inside the polish */
   float polish_tol;       /* relative KKT tolerance for accepting the polished point */
+  int32_t polish_repairs; /* active-set repairs (add violated / drop negative-multiplier faces
+                             and re-polish) before resuming ADMM */
   int64_t max_batch;      /* largest B passed to cmpc_solve (sizes plan workspace) */
 } cmpc_params;
 

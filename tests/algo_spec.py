@@ -14,7 +14,7 @@ F32 = np.float32
 class Params:
     def __init__(self, N=16, Q=None, R=None, mu=0.8, fz_min=10.0, rho=1e-4, sigma=1e-6,
                  alpha=1.6, max_iter=400, stable_checks=3, adaptive_interval=25,
-                 eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5):
+                 eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=3):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -24,6 +24,7 @@ class Params:
         self.adaptive_interval = adaptive_interval
         self.eps_abs, self.eps_rel = eps_abs, eps_rel
         self.polish_refine, self.tol_polish = polish_refine, tol_polish
+        self.repairs = repairs
 
 
 def project(v, mu, fz_min):
@@ -177,12 +178,13 @@ def solve(inst, p: Params):
         gs = F32(max(np.max(np.abs(g[fidx])), 1e-30))
         us = F32(max(np.max(np.abs(u)), 1.0))
         ok = bool(step <= p.tol_polish * us)
+        newcode = code.copy()
         ti = 0
         for k in range(N):
             for l in range(4):
                 if not stance[k, l]:
                     continue
-                c = code[ti]; ti += 1
+                c = code[ti]
                 b = 12 * k + 3 * l
                 sx = 1 if c & 2 else (-1 if c & 4 else 0)
                 sy = 1 if c & 8 else (-1 if c & 16 else 0)
@@ -192,17 +194,26 @@ def solve(inst, p: Params):
                 l0 = g[b + 2] - p.mu * (lx + ly)
                 tol_d = p.tol_polish * gs
                 tol_p = p.tol_polish * us
-                if sx and lx < -tol_d: ok = False
-                if sy and ly < -tol_d: ok = False
-                if (c & 1) and l0 < -tol_d: ok = False
-                if not sx and abs(fx) > p.mu * fz + tol_p: ok = False
-                if not sy and abs(fy) > p.mu * fz + tol_p: ok = False
-                if not (c & 1) and fz < p.fz_min - tol_p: ok = False
+                nc = c
+                if sx and lx < -tol_d: ok = False; nc &= ~6
+                if sy and ly < -tol_d: ok = False; nc &= ~24
+                if (c & 1) and l0 < -tol_d: ok = False; nc &= ~1
+                if not sx and abs(fx) > p.mu * fz + tol_p: ok = False; nc |= (2 if fx > 0 else 4)
+                if not sy and abs(fy) > p.mu * fz + tol_p: ok = False; nc |= (8 if fy > 0 else 16)
+                if not (c & 1) and fz < p.fz_min - tol_p: ok = False; nc |= 1
+                newcode[ti] = nc
+                ti += 1
+        self_newcode[0] = newcode
         return ok, u
+
+    self_newcode = [None]
 
     rho = p.rho
     L = admm_matrix(rho)
     x = np.zeros(nf, F32); z = np.zeros(nf, F32); y = np.zeros(nf, F32)
+    g0, _ = gradient(A, B, d, p.Q, p.R, full(x))
+    g0 = g0.reshape(-1)[fidx]               # = q of the condensed QP (gradient at 0)
+    nq = float(np.max(np.abs(g0), initial=0.0))
     prev_code = None; stable = 0
     status = -2; it = 0; U = None
     for it in range(1, p.max_iter + 1):
@@ -223,13 +234,22 @@ def solve(inst, p: Params):
         prev_code = code
         if stable >= p.stable_checks:
             ok, u = polish(z, code)
+            rep = 0
+            while not ok and rep < p.repairs:
+                c2 = self_newcode[0]
+                if np.array_equal(c2, code):
+                    break
+                code = c2
+                ok, u = polish(z, code)
+                rep += 1
             stable = -p.stable_checks  # back off before the next attempt
             if ok:
                 status = 1; U = u; break
         if p.adaptive_interval and it % p.adaptive_interval == 0:
             rp = np.max(np.abs(x - z)); rd = np.max(np.abs(g + y))
             npn = max(np.max(np.abs(x)), np.max(np.abs(z)), 1e-30)
-            nd = max(np.max(np.abs(g)), np.max(np.abs(y)), 1e-30)
+            # OSQP normalisation max(|P x|, |q|, |y|), with |P x| <= |g| + |q| approximated
+            nd = max(np.max(np.abs(g)), nq, np.max(np.abs(y)), 1e-30)
             nr = rho * np.sqrt((rp / npn) / (rd / nd + 1e-30))
             nr = min(max(nr, 1e-6), 1e6)
             if nr > 5 * rho or nr < rho / 5:
