@@ -1,5 +1,6 @@
 // cmpc_host.hip -- C-ABI (include/cmpc.h): plan management and kernel launches.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -11,7 +12,7 @@
 #include "cmpc.h"
 #include "cmpc_device.h"
 
-#include "cmpc_kernels.hip"  // kernels: same translation unit
+#include "cmpc_wave.hip"  // kernels: same translation unit
 
 struct cmpc_plan {
   cmpc_params p;
@@ -157,6 +158,12 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bin_fn(q), pl->threads[q], 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
+#ifdef CMPC_STAMPS
+    if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
+      const int c = atoi(cap);
+      if (c >= 1 && c < nb) nb = c;
+    }
+#endif
     pl->grid[q] = nb * cus;
     const size_t need = (size_t)pl->grid[q] * bin_slab(q);
     if (need > work_floats) work_floats = need;

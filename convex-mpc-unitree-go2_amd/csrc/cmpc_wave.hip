@@ -1,0 +1,1097 @@
+// cmpc_wave.hip -- batched convex-MPC contact-force QP solver for MI355X (gfx950):
+// ONE WAVEFRONT PER QP INSTANCE.
+//
+// Each 64-lane wave solves one QP of the reference's centroidal MPC
+// (convex_mpc/centroidal_mpc.py:69-359) with no workgroup barrier anywhere: the workgroup is the
+// wave, all cross-lane traffic is wave-ordered LDS or DPP, and a CU keeps 8 independent QPs in
+// flight (2 per SIMD) so one QP's latency is hidden behind another's MFMA/VALU work.
+// Algorithm (DESIGN.md "Kernel"):
+//
+//   1. Condense the horizon onto the free (stance) forces: H = 2 G'QG + 2R via the backward
+//      recursion S_j = Q2 + A'S_{j+1}A, W_jj = S_j B_j, W_ij = A'W_{i+1,j}, H_ij = B_i'W_ij, every
+//      12x12 product a chain of four v_mfma_f32_16x16x4_f32 whose accumulator is the next
+//      product's B operand.  H blocks are scattered into a per-wave global image laid out as the
+//      MFMA accumulator tiles (L2-resident), then loaded back as 16x16 tiles: lane (g, c)
+//      holds rows 4g..4g+3, column c of every lower-triangle tile (f4 per tile, in registers).
+//   2. Invert H + diag(R) + shift in registers by the BLOCK sweep operator, four pivots at a
+//      time: S <- S - P^ D^-1 P^' (P^ = the four pivot columns with the pivot block minus I),
+//      then -2 on the four pivot diagonals; the rank-4 update of each tile is ONE MFMA
+//      (A = -Y rows, B = diag(1/dl) Y' columns, Y = P^ L^-T from the 4x4 LDL' of the pivot
+//      block, factored redundantly per lane); pivot columns go through a 4-column LDS panel.
+//   3. ADMM (OSQP iteration, A = I) on the free forces, lane t owning stance triple t
+//      {fz >= fz_min, |fx| <= mu fz, |fy| <= mu fz} (closed-form projection).  Defect-correction
+//      x-update x~ = x + M(rho(z - x) - grad f(x) - y): M (fp32 inverse) preconditions, grad f
+//      comes from the error-coordinate rollout/adjoint (e_{k+1} = A e_k + B_k u_k + d_k).
+//   4. Active-set polish once the face pattern is stable: reduced basis u = T v + t0, condense
+//      + invert again (the ADMM inverse is parked in a per-wave global slab), refine with the
+//      exact gradient, KKT check, primal-dual repairs of the face set.
+//
+// Instances are binned by free-variable count (NC in {96,128,160,192}, a multiple of 16);
+// each bin runs a persistent kernel whose waves pull instance ids from a device-side queue.
+//
+// This file is compiled as part of cmpc_host.hip (single translation unit).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cmpc_device.h"
+
+namespace cmpc {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------
+// wave helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// v[l] and v[l ^ 32] (resp. v[l ^ 16]) without address registers (gfx950 permlane swaps):
+// after the swap the two results hold the lane's own value and its partner's in some order
+__device__ __forceinline__ void pair32(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  a = __int_as_float(r[0]);
+  b = __int_as_float(r[1]);
+}
+__device__ __forceinline__ void pair16(float v, float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  a = __int_as_float(r[0]);
+  b = __int_as_float(r[1]);
+}
+
+// max over the wave, result in every lane
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dpp<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dpp<0x141>(v));  // row_half_mirror
+  v = fmaxf(v, dpp<0x140>(v));  // row_mirror
+  float a, b;
+  pair32(v, a, b);
+  v = fmaxf(a, b);
+  pair16(v, a, b);
+  return fmaxf(a, b);
+}
+
+// exclusive prefix sum of small non-negative counts (< 4) across the wave
+__device__ __forceinline__ int wave_excl_scan4(int v) {
+  const unsigned long long b0 = __ballot(v & 1), b1 = __ballot(v & 2);
+  const int c0 = __builtin_amdgcn_mbcnt_hi((unsigned)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b0, 0));
+  const int c1 = __builtin_amdgcn_mbcnt_hi((unsigned)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b1, 0));
+  return c0 + 2 * c1;
+}
+__device__ __forceinline__ int wave_total4(int v) {
+  return __popcll(__ballot(v & 1)) + 2 * __popcll(__ballot(v & 2));
+}
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// sum over the 16 lanes of a DPP row (lanes with equal lane>>4), result in every lane
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0x141>(v);  // row_half_mirror
+  v += dpp<0x140>(v);  // row_mirror
+  return v;
+}
+
+// sum over the 4 rows (lanes c, c+16, c+32, c+48), result in every lane
+__device__ __forceinline__ float col4_sum(float v) {
+  float a, b;
+  pair32(v, a, b);
+  pair16(a + b, a, b);
+  return a + b;
+}
+
+// Lane id the compiler cannot see as loop invariant: every phase re-derives its lane-dependent
+// addresses locally instead of the persistent loops hoisting them (and spilling them) for the
+// whole instance.
+__device__ __forceinline__ int opaque_lane() {
+  int l = threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+
+// Order LDS traffic between lanes of the wave: DS instructions of one wave execute in order,
+// so only the compiler must not move memory operations across this point.
+#define WSYNC() asm volatile("" ::: "memory")
+
+// ------------------------------------------------------------------------------------------
+// diagnostic build only (-DCMPC_STAMPS): per-phase s_memtime cycle totals.  Phases: 0 condense
+// (+tile load), 1 invert, 2 gradient, 3 symv, 4 polish (all of it), 5 instance total,
+// 6 condense MFMA+scatter only; counters: 8 condense+invert calls, 9 polish attempts,
+// 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls.
+// ------------------------------------------------------------------------------------------
+#ifdef CMPC_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define CMPC_T0(name) const unsigned long long name = __builtin_amdgcn_s_memtime()
+#define CMPC_ACC(ph, t0)                                                              \
+  do {                                                                                \
+    const unsigned long long _t1 = __builtin_amdgcn_s_memtime();                      \
+    if (threadIdx.x == 0) atomicAdd(&g_stamps[ph], _t1 - (t0));                       \
+  } while (0)
+#define CMPC_CNT(ph, v) \
+  do { if (threadIdx.x == 0) atomicAdd(&g_stamps[ph], (unsigned long long)(v)); } while (0)
+#else
+#define CMPC_T0(name) (void)0
+#define CMPC_ACC(ph, t0) (void)0
+#define CMPC_CNT(ph, v) (void)0
+#endif
+
+// ------------------------------------------------------------------------------------------
+// geometry and LDS image of one instance
+// ------------------------------------------------------------------------------------------
+constexpr int kMaxN = 16;
+constexpr int kMaxP = 12 * kMaxN;   // 192
+constexpr int kMaxTri = 4 * kMaxN;  // 64 = lanes: lane t owns stance triple t
+
+template <int NC>
+struct Cfg {
+  static_assert(NC % 16 == 0, "bin capacity must be a multiple of 16");
+  static constexpr int TT = NC / 16;             // 16x16 tile rows
+  static constexpr int NTL = TT * (TT + 1) / 2;  // lower-triangle tiles (f4 per lane each)
+  static constexpr int THREADS = 64;             // one wave per QP
+  static constexpr int IMG = NTL * 256;          // floats of one tile image
+  static constexpr int SLAB = 2 * IMG;           // per wave: condensation image + park slab
+  // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
+  static constexpr int WPE = (4 * NTL <= 150) ? 2 : 1;
+};
+
+template <int NC>
+struct Smem {
+  alignas(16) float Bt[NC * 12];   // param-space input matrix, column p at Bt[12p .. 12p+11]
+  alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
+  alignas(16) float x[NC];
+  alignas(16) float z[NC];
+  alignas(16) float g[NC];
+  alignas(16) float r[NC];
+  alignas(16) float v[NC];
+  alignas(16) float dl[NC];
+  alignas(16) float ds[NC];        // unit-diagonal scaling of the sweep
+  alignas(16) float pan[NC * 4];   // sweep panel: 4 pivot columns, row-major [row][4]
+  float D[kMaxP];                  // d_k  (error-coordinate affine term)
+  float Dt[kMaxP];                 // d~_k (d_k + B_k t0_k in the polish basis)
+  float H[kMaxP];                  // h_k = B~_k v_k + d~_k
+  float E[kMaxP];                  // e_{k+1} = x_{k+1} - xref_k
+  float L[kMaxP];                  // lambda_k
+  float A[144];
+  float Q2[12];                    // KParams copies (indexed at run time -> keep out of kernarg)
+  float R2[12];
+  int par[NC];                     // param -> step k
+  int off[kMaxN + 1];              // first param of step k
+  int tri[kMaxTri];                // stance triple t -> 4k + leg
+  int tri_of[kMaxTri];             // 4k + leg -> triple index or -1
+  int tcnt[kMaxTri];               // polish: params of triple t / repaired face code
+  int code[kMaxTri];               // face code of triple t
+};
+
+__device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * (I + 1)) / 2 + J; }
+
+// ------------------------------------------------------------------------------------------
+// condensation (MFMA) -> per-wave tile image (global, lower triangle, accumulator layout)
+// ------------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ f4 load_bcol(const Smem<NC>& s, int p0, int m, int g, int c) {
+  f4 v = {0.f, 0.f, 0.f, 0.f};
+  if (c < m && g < 3) v = *reinterpret_cast<const f4*>(&s.Bt[(p0 + c) * 12 + 4 * g]);
+  return v;
+}
+
+// element (p, q), p >= q, of the symmetric matrix -> image float index
+__device__ __forceinline__ int img_index(int p, int q) {
+  const int r = p & 15, c = q & 15;
+  return tile_index(p >> 4, q >> 4) * 256 + ((r >> 2) * 16 + c) * 4 + (r & 3);
+}
+
+template <int NC>
+__device__ __forceinline__ void condense_image(Smem<NC>& s, const KParams& P,
+                                               float* __restrict__ img) {
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int N = P.N;
+  float Ar[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = 4 * g + q;
+    Ar[q] = (row < 12 && c < 12) ? s.A[row * 12 + c] : 0.f;
+  }
+  f4 S;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = 4 * g + q;
+    S[q] = (row < 12 && row == c) ? s.Q2[row] : 0.f;
+  }
+  for (int j = N - 1; j >= 0; --j) {
+    if (j < N - 1) {  // S_j = Q2 + A' (S_{j+1} A)
+      f4 T1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) T1 = mfma4(S[q], Ar[q], T1);
+      f4 Sn = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Sn = mfma4(Ar[q], T1[q], Sn);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 4 * g + q;
+        if (row < 12 && row == c) Sn[q] += s.Q2[row];
+      }
+      S = Sn;
+    }
+    const int pj0 = s.off[j], mj = s.off[j + 1] - pj0;
+    if (mj == 0) continue;
+    const f4 bj = load_bcol(s, pj0, mj, g, c);
+    f4 W = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) W = mfma4(S[q], bj[q], W);
+    for (int i = j; i >= 0; --i) {
+      if (i < j) {  // W <- A' W
+        f4 Wn = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Wn = mfma4(Ar[q], W[q], Wn);
+        W = Wn;
+      }
+      const int pi0 = s.off[i], mi = s.off[i + 1] - pi0;
+      if (mi == 0) continue;
+      const f4 bi = load_bcol(s, pi0, mi, g, c);
+      f4 Hb = {0.f, 0.f, 0.f, 0.f};  // Hb[q] = H[pi0 + 4g+q][pj0 + c]
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Hb = mfma4(bi[q], W[q], Hb);
+      const int p = pj0 + c;  // lower triangle: row p >= column qc
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int qq = 4 * g + q, qc = pi0 + qq;
+        if (qq < mi && c < mj && (i != j || c >= qq)) {
+          img[img_index(p, qc)] = Hb[q];
+          if ((p >> 4) == (qc >> 4) && p != qc) img[img_index(qc, p)] = Hb[q];
+        }
+      }
+    }
+  }
+}
+
+// register tiles <- image, + diag(Rt) + shift, identity on padding
+template <int NC>
+__device__ __forceinline__ void load_tiles(f4 (&M)[Cfg<NC>::NTL], const Smem<NC>& s,
+                                           const float* __restrict__ img, int n, float shift) {
+  using C = Cfg<NC>;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int TA = (n + 15) >> 4;
+  // own stores of this wave are in L2; drop any stale L1 copy of the image before reading
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      const int t = tile_index(I, J);
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (I < TA) v = *reinterpret_cast<const f4*>(&img[t * 256 + lane * 4]);
+      const int col = 16 * J + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
+        else if (row == col) v[q] += s.Rt[row] + shift;
+      }
+      M[t] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// block sweep inversion (4 pivots per step, MFMA rank-4 updates)
+// ------------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL], int n) {
+  using C = Cfg<NC>;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int TA = (n + 15) >> 4;
+  // unit-diagonal scaling (padding: 1)
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    const f4 d = M[tile_index(I, I)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int p = 16 * I + c;
+      if (4 * g + q == c) s.ds[p] = (p < n && d[q] > 0.f) ? rsqrtf(d[q]) : 1.f;
+    }
+  }
+  WSYNC();
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    const f4 ri = *reinterpret_cast<const f4*>(&s.ds[16 * I + 4 * g]);
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      const float cj = s.ds[16 * J + c];
+      f4& m = M[tile_index(I, J)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
+    }
+  }
+  const int ng = (n + 3) >> 2;
+  for (int st = 0; st < ng; ++st) {
+    const int k0 = 4 * st, K = k0 >> 4, c0 = k0 & 15, gp = c0 >> 2;
+    // publish the 4 pivot columns (current values) as panel rows [row][0..3]
+#pragma unroll
+    for (int I = 0; I < C::TT; ++I) {
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const f4 m = M[tile_index(I, J)];
+        if (J == K && I < TA) {  // column part: rows 16I + 4g + q, panel column c - c0
+          const int pc = c - c0;
+          if (pc >= 0 && pc < 4) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
+          }
+        }
+        if (I == K && J < K) {  // row part (transposed): rows k0..k0+3 of tile (K, J)
+          if (g == gp) *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = m;
+        }
+      }
+    }
+    WSYNC();
+    // D = L diag(dl) L' (unit lower L), so P^ D^-1 P^' = Y diag(1/dl) Y' with Y = P^ L^-T: the
+    // columns of Y are the pivot columns as the scalar sweep would see them (each already
+    // eliminated by the earlier pivots of the step), which keeps the scalar sweep's accuracy.
+    float Dm[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f4 rrow = *reinterpret_cast<const f4*>(&s.pan[(k0 + i) * 4]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j];
+    }
+    const float d0 = Dm[0];
+    const float i0 = __builtin_amdgcn_rcpf(d0);
+    const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
+    const float d1 = Dm[5] - l10 * Dm[4];
+    const float i1 = __builtin_amdgcn_rcpf(d1);
+    const float l21 = (Dm[9] - l20 * Dm[4]) * i1;
+    const float l31 = (Dm[13] - l30 * Dm[4]) * i1;
+    const float d2 = Dm[10] - l20 * Dm[8] - l21 * (Dm[9] - l20 * Dm[4]);
+    const float i2 = __builtin_amdgcn_rcpf(d2);
+    const float l32 = (Dm[14] - l30 * Dm[8] - l31 * (Dm[9] - l20 * Dm[4])) * i2;
+    const float d3 = Dm[15] - l30 * Dm[12] - l31 * (Dm[13] - l30 * Dm[4]) -
+                     l32 * (Dm[14] - l30 * Dm[8] - l31 * (Dm[9] - l20 * Dm[4]));
+    const float i3 = __builtin_amdgcn_rcpf(d3);
+    const float ig = (g == 0) ? i0 : (g == 1) ? i1 : (g == 2) ? i2 : i3;
+    float a[C::TT], b[C::TT];
+#pragma unroll
+    for (int I = 0; I < C::TT; ++I) {
+      if (I < TA) {
+        const int row = 16 * I + c;
+        const f4 pr = *reinterpret_cast<const f4*>(&s.pan[row * 4]);
+        float ph[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ph[m] = pr[m] - ((row == k0 + m) ? 1.f : 0.f);
+        const float y0 = ph[0];
+        const float y1 = ph[1] - l10 * y0;
+        const float y2 = ph[2] - l20 * y0 - l21 * y1;
+        const float y3 = ph[3] - l30 * y0 - l31 * y1 - l32 * y2;
+        const float yg = (g == 0) ? y0 : (g == 1) ? y1 : (g == 2) ? y2 : y3;
+        a[I] = -yg;
+        b[I] = yg * ig;
+      } else {
+        a[I] = 0.f;
+        b[I] = 0.f;
+      }
+    }
+#pragma unroll
+    for (int I = 0; I < C::TT; ++I) {
+      if (I >= TA) continue;  // uniform
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        const int t = tile_index(I, J);
+        M[t] = mfma4(a[I], b[J], M[t]);
+      }
+    }
+#pragma unroll
+    for (int I = 0; I < C::TT; ++I) {
+      if (I == K) {
+        f4& m = M[tile_index(I, I)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (g == gp && c == c0 + q) m[q] -= 2.f;
+      }
+    }
+  }
+  // M holds -(scaled inverse): undo sign and scaling
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    const f4 ri = *reinterpret_cast<const f4*>(&s.ds[16 * I + 4 * g]);
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      const float cj = -s.ds[16 * J + c];
+      f4& m = M[tile_index(I, J)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
+    }
+  }
+}
+
+// out = M in over the first n params (M in register tiles, symmetric, lower triangle stored);
+// `in` must be zero for n <= p < NC
+template <int NC>
+__device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], int n,
+                                     const float* in, float* out) {
+  using C = Cfg<NC>;
+  CMPC_T0(t_sv);
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int TA = (n + 15) >> 4;
+  WSYNC();
+  float xc[C::TT], cacc[C::TT];
+#pragma unroll
+  for (int J = 0; J < C::TT; ++J) {
+    xc[J] = in[16 * J + c];
+    cacc[J] = 0.f;
+  }
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    if (I >= TA) {  // padding rows: zero (uniform branch)
+      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = f4{0.f, 0.f, 0.f, 0.f};
+      continue;
+    }
+    const f4 xr = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
+    f4 racc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      const f4 m = M[tile_index(I, J)];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) racc[q] = fmaf(m[q], xc[J], racc[q]);
+      if (J < I) {
+        float cs = cacc[J];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cs = fmaf(m[q], xr[q], cs);
+        cacc[J] = cs;
+      }
+    }
+    // row sums over the 16 lanes of each DPP row -> out rows 16I + 4g + q
+    f4 rs;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) rs[q] = row16_sum(racc[q]);
+    if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = rs;
+  }
+  WSYNC();
+#pragma unroll
+  for (int J = 0; J < C::TT; ++J) {
+    if (J >= TA) continue;
+    const float cs = col4_sum(cacc[J]);
+    if (g == 0) out[16 * J + c] += cs;
+  }
+  WSYNC();
+  CMPC_ACC(3, t_sv);
+  CMPC_CNT(13, 1);
+}
+
+// Gradient of sum_k e_{k+1}'(Q2/2)e_{k+1} + v'(Rt/2)v in the current param basis
+// (e by the error-coordinate rollout).  Leaves E (e_{k+1}) and L (lambda_k) in LDS.
+template <int NC>
+__device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, const float* vin,
+                                         float* gout) {
+  CMPC_T0(t_gr);
+  const int lane = opaque_lane();
+  const int N = P.N;
+  const int NP = 12 * N;
+  WSYNC();
+  for (int o = lane; o < NP; o += 64) {  // h_k = B~_k v_k + d~_k
+    const int k = o / 12, r = o % 12;
+    float acc = s.Dt[o];
+    for (int p = s.off[k]; p < s.off[k + 1]; ++p) acc = fmaf(s.Bt[p * 12 + r], vin[p], acc);
+    s.H[o] = acc;
+  }
+  WSYNC();
+  {  // sequential recursions (lanes 0..11 carry the state)
+    const int i = lane % 12;
+    float Arow[12], Acol[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      Arow[j] = s.A[i * 12 + j];
+      Acol[j] = s.A[j * 12 + i];
+    }
+    float e = 0.f;
+    for (int k = 0; k < N; ++k) {  // e_{k+1} = A e_k + h_k
+      float a0 = s.H[12 * k + i], a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 12; j += 3) {
+        a0 = fmaf(Arow[j], readlane_f(e, j), a0);
+        a1 = fmaf(Arow[j + 1], readlane_f(e, j + 1), a1);
+        a2 = fmaf(Arow[j + 2], readlane_f(e, j + 2), a2);
+      }
+      e = a0 + (a1 + a2);
+      if (lane < 12) s.E[12 * k + i] = e;
+    }
+    float lam = 0.f;
+    const float q2 = s.Q2[i];
+    WSYNC();
+    for (int k = N - 1; k >= 0; --k) {  // lambda_k = Q2 e_{k+1} + A' lambda_{k+1}
+      float a0 = q2 * s.E[12 * k + i], a1 = 0.f, a2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 12; j += 3) {
+        a0 = fmaf(Acol[j], readlane_f(lam, j), a0);
+        a1 = fmaf(Acol[j + 1], readlane_f(lam, j + 1), a1);
+        a2 = fmaf(Acol[j + 2], readlane_f(lam, j + 2), a2);
+      }
+      lam = a0 + (a1 + a2);
+      if (lane < 12) s.L[12 * k + i] = lam;
+    }
+  }
+  WSYNC();
+  for (int p = lane; p < n; p += 64) {  // g = B~' lambda + Rt v
+    const int k = s.par[p];
+    const f4* bt = reinterpret_cast<const f4*>(&s.Bt[p * 12]);
+    const f4* l = reinterpret_cast<const f4*>(&s.L[12 * k]);
+    float acc = s.Rt[p] * vin[p];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const f4 lv = l[j], bv = bt[j];
+      acc = fmaf(bv[0], lv[0], acc); acc = fmaf(bv[1], lv[1], acc);
+      acc = fmaf(bv[2], lv[2], acc); acc = fmaf(bv[3], lv[3], acc);
+    }
+    gout[p] = acc;
+  }
+  WSYNC();
+  CMPC_ACC(2, t_gr);
+  CMPC_CNT(12, 1);
+}
+
+// Euclidean projection of (a, b, c) onto {|x| <= mu z, |y| <= mu z, z >= fz_min}.
+// Face code bits: 1 fz at fz_min, 2/4 fx at +/-mu fz, 8/16 fy at +/-mu fz.
+__device__ __forceinline__ int project(float a, float b, float c, float mu, float fzmin,
+                                       float& px, float& py, float& pz) {
+  const float Aa = fabsf(a), Bb = fabsf(b);
+  const float lo = fminf(Aa, Bb), hi = fmaxf(Aa, Bb);
+  const float z1 = (c + mu * (Aa + Bb)) / (1.f + 2.f * mu * mu);
+  const float z2 = (c + mu * hi) / (1.f + mu * mu);
+  float zz = (mu * z1 < lo) ? z1 : ((mu * z2 < hi) ? z2 : c);
+  int code = 0;
+  if (zz < fzmin) { zz = fzmin; code |= 1; }
+  const float lim = mu * zz;
+  if (a > lim) { px = lim; code |= 2; } else if (a < -lim) { px = -lim; code |= 4; } else px = a;
+  if (b > lim) { py = lim; code |= 8; } else if (b < -lim) { py = -lim; code |= 16; } else py = b;
+  pz = zz;
+  return code;
+}
+
+// ADMM basis: every stance triple contributes (fx, fy, fz) as params 3t, 3t+1, 3t+2
+template <int NC>
+__device__ __forceinline__ void build_admm_basis(Smem<NC>& s, const KParams& P,
+                                                 const float* __restrict__ Bg, int ntri) {
+  const int lane = opaque_lane();
+  const int N = P.N;
+  const int n = 3 * ntri;
+  WSYNC();
+  for (int e = lane; e < n * 12; e += 64) {
+    const int p = e / 12, r = e % 12;
+    const int t = p / 3, a = p % 3;
+    const int kl = s.tri[t];
+    const int k = kl >> 2, leg = kl & 3;
+    s.Bt[e] = Bg[(k * 12 + r) * 12 + 3 * leg + a];
+  }
+  for (int p = lane; p < NC; p += 64) {
+    if (p < n) {
+      const int t = p / 3, a = p % 3;
+      const int kl = s.tri[t];
+      s.Rt[p] = s.R2[3 * (kl & 3) + a];
+      s.par[p] = kl >> 2;
+    } else {
+      s.Rt[p] = 0.f;
+      s.par[p] = 0;
+      s.x[p] = 0.f; s.z[p] = 0.f; s.g[p] = 0.f; s.r[p] = 0.f;
+      s.v[p] = 0.f; s.dl[p] = 0.f;
+    }
+  }
+  for (int k = lane; k <= N; k += 64) {
+    int c = 0;
+    for (int t = 0; t < ntri; ++t) c += ((s.tri[t] >> 2) < k) ? 1 : 0;
+    s.off[k] = 3 * c;
+  }
+  for (int o = lane; o < 12 * N; o += 64) s.Dt[o] = s.D[o];
+  WSYNC();
+}
+
+// Polish setup: the reduced basis of the faces in s.code (lane t owns triple t),
+// u = T v + t0 with t0 = locked components, v initialised from z.  Returns nr.
+struct TripleFaces {
+  int k, leg, sx, sy, px, py, pz;
+  bool zl, owns;
+};
+
+template <int NC>
+__device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
+                                            const float* __restrict__ Bg, int ntri,
+                                            TripleFaces& tf) {
+  const int lane = opaque_lane();
+  const int N = P.N;
+  const float mu = P.mu, fzmin = P.fz_min;
+  tf = TripleFaces{0, 0, 0, 0, -1, -1, -1, false, false};
+  WSYNC();
+  tf.owns = lane < ntri;
+  const int code = tf.owns ? s.code[lane] : 0;
+  const int kl = tf.owns ? s.tri[lane] : 0;
+  const int k = kl >> 2, leg = kl & 3;
+  const int sx = (code & 2) ? 1 : ((code & 4) ? -1 : 0);
+  const int sy = (code & 8) ? 1 : ((code & 16) ? -1 : 0);
+  const bool zl = (code & 1) != 0;
+  tf.k = k; tf.leg = leg; tf.sx = sx; tf.sy = sy; tf.zl = zl;
+  const int cnt = tf.owns ? ((sx == 0) + (sy == 0) + (!zl)) : 0;
+  const int base = wave_excl_scan4(cnt);
+  const int nr = wave_total4(cnt);
+  const float* Bk = Bg + k * 144;
+  if (tf.owns) {
+    s.tcnt[lane] = cnt;
+    int p = base;
+    if (sx == 0) {
+      tf.px = p++;
+      for (int r = 0; r < 12; ++r) s.Bt[tf.px * 12 + r] = Bk[r * 12 + 3 * leg];
+      s.Rt[tf.px] = s.R2[3 * leg];
+      s.par[tf.px] = k;
+      s.v[tf.px] = s.z[3 * lane];
+    }
+    if (sy == 0) {
+      tf.py = p++;
+      for (int r = 0; r < 12; ++r) s.Bt[tf.py * 12 + r] = Bk[r * 12 + 3 * leg + 1];
+      s.Rt[tf.py] = s.R2[3 * leg + 1];
+      s.par[tf.py] = k;
+      s.v[tf.py] = s.z[3 * lane + 1];
+    }
+    if (!zl) {
+      tf.pz = p++;
+      const float cx = sx * mu, cy = sy * mu;
+      for (int r = 0; r < 12; ++r)
+        s.Bt[tf.pz * 12 + r] = Bk[r * 12 + 3 * leg + 2] + cx * Bk[r * 12 + 3 * leg] +
+                               cy * Bk[r * 12 + 3 * leg + 1];
+      s.Rt[tf.pz] = s.R2[3 * leg + 2] + mu * mu * ((sx != 0 ? s.R2[3 * leg] : 0.f) +
+                                                   (sy != 0 ? s.R2[3 * leg + 1] : 0.f));
+      s.par[tf.pz] = k;
+      s.v[tf.pz] = s.z[3 * lane + 2];
+    }
+  }
+  WSYNC();
+  for (int kk = lane; kk <= N; kk += 64) {
+    int c = 0;
+    for (int t = 0; t < ntri; ++t) c += ((s.tri[t] >> 2) < kk) ? s.tcnt[t] : 0;
+    s.off[kk] = c;
+  }
+  for (int o = lane; o < 12 * N; o += 64) {  // d~ = d + B t0 (fz locked at fz_min)
+    const int kk = o / 12, r = o % 12;
+    float acc = s.D[o];
+    for (int l = 0; l < 4; ++l) {
+      const int t = s.tri_of[4 * kk + l];
+      if (t < 0) continue;
+      const int c = s.code[t];
+      if (!(c & 1)) continue;
+      const float tx = (c & 2) ? mu * fzmin : ((c & 4) ? -mu * fzmin : 0.f);
+      const float ty = (c & 8) ? mu * fzmin : ((c & 16) ? -mu * fzmin : 0.f);
+      const float* Bkk = Bg + kk * 144 + r * 12 + 3 * l;
+      acc = fmaf(Bkk[0], tx, acc);
+      acc = fmaf(Bkk[1], ty, acc);
+      acc = fmaf(Bkk[2], fzmin, acc);
+    }
+    s.Dt[o] = acc;
+  }
+  for (int p = lane; p < NC; p += 64)
+    if (p >= nr) { s.v[p] = 0.f; s.g[p] = 0.f; s.dl[p] = 0.f; }
+  WSYNC();
+  return nr;
+}
+
+// Polish check after refinement (E, L at the final v in LDS): KKT conditions per triple.
+// On success the triple's force is returned in (fx, fy, fz); the repaired face code of a
+// failing triple is left in s.tcnt.  Returns (all ok, any face changed) via `changed`.
+template <int NC>
+__device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
+                                             const float* __restrict__ Bg, const TripleFaces& tf,
+                                             float step, float& fx, float& fy, float& fz,
+                                             bool& changed) {
+  const int lane = opaque_lane();
+  const float mu = P.mu, fzmin = P.fz_min;
+  fx = 0.f; fy = 0.f; fz = 0.f;
+  float gx = 0.f, gy = 0.f, gz = 0.f;
+  const int k = tf.k, leg = tf.leg, sx = tf.sx, sy = tf.sy;
+  WSYNC();
+  if (tf.owns) {
+    fz = tf.zl ? fzmin : s.v[tf.pz];
+    fx = (sx == 0) ? s.v[tf.px] : sx * mu * fz;
+    fy = (sy == 0) ? s.v[tf.py] : sy * mu * fz;
+    const float* Bk = Bg + k * 144;
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    for (int r = 0; r < 12; ++r) {
+      const float lr = s.L[12 * k + r];
+      ax = fmaf(Bk[r * 12 + 3 * leg], lr, ax);
+      ay = fmaf(Bk[r * 12 + 3 * leg + 1], lr, ay);
+      az = fmaf(Bk[r * 12 + 3 * leg + 2], lr, az);
+    }
+    gx = ax + s.R2[3 * leg] * fx;
+    gy = ay + s.R2[3 * leg + 1] * fy;
+    gz = az + s.R2[3 * leg + 2] * fz;
+  }
+  const float gs = wave_max(fmaxf(fabsf(gx), fmaxf(fabsf(gy), fabsf(gz))));
+  const float us = wave_max(fmaxf(1.f, fmaxf(fabsf(fx), fmaxf(fabsf(fy), fabsf(fz)))));
+  const float tol_d = P.polish_tol * gs, tol_p = P.polish_tol * us;
+  bool ok = true;
+  int nc = 0;
+  if (tf.owns) {
+    // KKT per triple; on a violation also derive the repaired face set (primal-dual
+    // active-set step): drop faces with a negative multiplier, add violated faces
+    const float lx = sx ? -sx * gx : 0.f;
+    const float ly = sy ? -sy * gy : 0.f;
+    const float l0 = gz - mu * (lx + ly);
+    nc = s.code[lane];
+    if (sx && lx < -tol_d) { ok = false; nc &= ~6; }
+    if (sy && ly < -tol_d) { ok = false; nc &= ~24; }
+    if (tf.zl && l0 < -tol_d) { ok = false; nc &= ~1; }
+    if (!sx && fabsf(fx) > mu * fz + tol_p) { ok = false; nc |= (fx > 0.f) ? 2 : 4; }
+    if (!sy && fabsf(fy) > mu * fz + tol_p) { ok = false; nc |= (fy > 0.f) ? 8 : 16; }
+    if (!tf.zl && fz < fzmin - tol_p) { ok = false; nc |= 1; }
+    if (!(isfinite(fx) && isfinite(fy) && isfinite(fz))) ok = false;
+    s.tcnt[lane] = nc;  // repaired code (copied into s.code by the caller if used)
+  }
+  changed = __any(tf.owns && nc != s.code[lane]) != 0;
+  return (__all(ok) != 0) && (step <= P.polish_tol * us);
+}
+
+// park / restore the register-resident inverse in the wave's global slab (uniform base,
+// 32-bit lane offset: no per-tile 64-bit address registers)
+template <int NC>
+__device__ __forceinline__ void park_store(float* __restrict__ park, const f4 (&M)[Cfg<NC>::NTL]) {
+  const int lane = opaque_lane();
+#pragma unroll
+  for (int t = 0; t < Cfg<NC>::NTL; ++t)
+    *reinterpret_cast<f4*>(&park[t * 256 + lane * 4]) = M[t];
+}
+
+template <int NC>
+__device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M)[Cfg<NC>::NTL]) {
+  const int lane = opaque_lane();
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < Cfg<NC>::NTL; ++t)
+    M[t] = *reinterpret_cast<const f4*>(&park[t * 256 + lane * 4]);
+}
+
+// ------------------------------------------------------------------------------------------
+// one QP instance on one wave
+// ------------------------------------------------------------------------------------------
+template <int NC>
+__device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
+                                               const Inputs& in, const Outputs& out,
+                                               float* __restrict__ img,
+                                               float* __restrict__ park) {
+  using C = Cfg<NC>;
+  f4 M[C::NTL];
+  const int lane = opaque_lane();
+  const int N = P.N;
+  const int NP = 12 * N;
+  const float* Ab = in.Ad + b * 144;
+  const float* Bg = in.Bd + b * (int64_t)N * 144;
+  const float* gdb = in.gd + b * 12;
+  const float* x0b = in.x0 + b * 12;
+  const float* xrb = in.xref + b * (int64_t)N * 12;
+  const uint8_t* ctb = in.contact + b * (int64_t)4 * N;
+  CMPC_T0(t_inst);
+  CMPC_CNT(10, 1);
+
+  WSYNC();
+  for (int e = lane; e < 144; e += 64) s.A[e] = Ab[e];
+  // stance triples in (k, leg) order; lane = 4k + leg
+  const bool stc = (lane < 4 * N) ? (ctb[(lane & 3) * N + (lane >> 2)] != 0) : false;
+  const int pos = wave_excl_scan4(stc ? 1 : 0);
+  const int ntri = wave_total4(stc ? 1 : 0);
+  if (stc) s.tri[pos] = lane;
+  if (lane < 4 * N) s.tri_of[lane] = stc ? pos : -1;
+  WSYNC();
+  for (int o = lane; o < NP; o += 64) {  // d_k = A r_k + gd - r_{k+1}, r_0 = x0
+    const int k = o / 12, r = o % 12;
+    const float* rk = (k == 0) ? x0b : (xrb + (k - 1) * 12);
+    float acc = gdb[r] - xrb[k * 12 + r];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc = fmaf(s.A[r * 12 + j], rk[j], acc);
+    s.D[o] = acc;
+  }
+  build_admm_basis<NC>(s, P, Bg, ntri);
+  const int n = 3 * ntri;
+  for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; }
+
+  // ADMM state of this lane's triple (params 3*lane + a), in registers
+  float xs[3] = {0.f, 0.f, 0.f}, zs[3] = {0.f, 0.f, 0.f}, ys[3] = {0.f, 0.f, 0.f};
+  const bool mine = lane < ntri;
+
+  int status = -2, iters = 0;
+  bool polished = false;
+  float pfx = 0.f, pfy = 0.f, pfz = 0.f;  // polished force of this lane's triple
+  TripleFaces tf;
+  float rho = P.rho0;
+  float rp = 0.f, rd = 0.f, np_ = 0.f, nd = 0.f;
+  int prev_code = -1, stable = 0;
+  bool refactor = n > 0;  // (re)build + invert the matrix for the current basis
+  bool in_polish = false;
+  int nact = n;           // params of the current basis
+  float shift = P.sigma + rho;
+  int it = 0;
+  int repairs_left = 0;
+  bool parked = false;    // the ADMM inverse is in the park slab
+  const float alpha = P.alpha;
+  if (n == 0) status = 1;
+  while (n > 0) {
+    if (refactor) {  // the only condense + invert call site
+      CMPC_CNT(8, 1);
+      CMPC_T0(t_c);
+      condense_image<NC>(s, P, img);
+      CMPC_ACC(6, t_c);
+      load_tiles<NC>(M, s, img, nact, shift);
+      CMPC_ACC(0, t_c);
+      CMPC_T0(t_i);
+      invert_tiles<NC>(s, M, nact);
+      CMPC_ACC(1, t_i);
+      refactor = false;
+    }
+    if (in_polish) {
+      CMPC_T0(t_pol);
+      float step = 3.0e38f;
+      for (int q = 0; q < P.polish_refine; ++q) {
+        gradient<NC>(s, P, nact, s.v, s.g);
+        symv<NC>(s, M, nact, s.g, s.dl);
+        float m = 0.f;
+        for (int p = lane; p < nact; p += 64) {
+          s.v[p] -= s.dl[p];
+          m = fmaxf(m, fabsf(s.dl[p]));
+        }
+        step = wave_max(m);
+      }
+      gradient<NC>(s, P, nact, s.v, s.g);  // E, L at the final point
+      bool changed = false;
+      const bool ok = polish_check<NC>(s, P, Bg, tf, step, pfx, pfy, pfz, changed);
+#ifdef CMPC_TRACE
+      if (b == CMPC_TRACE && lane == 0)
+        printf("it %d polish nact %d ok %d changed %d step %g repairs_left %d\n", it, nact, (int)ok,
+               (int)changed, step, repairs_left);
+#endif
+      CMPC_ACC(4, t_pol);
+      if (ok) {
+        polished = true;
+        status = 1;
+        break;
+      }
+      if (repairs_left > 0 && changed) {  // re-polish on the repaired face set
+        --repairs_left;
+        if (lane < ntri) s.code[lane] = s.tcnt[lane];
+        nact = polish_setup<NC>(s, P, Bg, ntri, tf);
+        shift = P.sigma;
+        refactor = true;
+        continue;
+      }
+      // restore the parked ADMM inverse (or rebuild it) and the basis, continue ADMM
+      if (parked) {
+        park_load<NC>(park, M);
+      } else {
+        refactor = true;
+      }
+      build_admm_basis<NC>(s, P, Bg, ntri);
+      if (mine) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { s.x[3 * lane + a] = xs[a]; s.z[3 * lane + a] = zs[a]; }
+      }
+      in_polish = false;
+      nact = n;
+      shift = P.sigma + rho;
+    }
+    if (it >= P.max_iter) break;
+    ++it;
+    iters = it;
+    // ---- one ADMM iteration ----
+    gradient<NC>(s, P, n, s.x, s.g);
+    if (mine) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int p = 3 * lane + a;
+        s.r[p] = rho * (zs[a] - xs[a]) - s.g[p] - ys[a];
+      }
+    }
+    symv<NC>(s, M, n, s.r, s.dl);
+    const bool last = (it == P.max_iter);
+    const bool adapt = P.adaptive_interval > 0 && (it % P.adaptive_interval) == 0;
+    const float inv_rho = 1.f / rho;
+    int code = 0;
+    float lrp = 0.f, lrd = 0.f, lnp = 0.f, lnd = 0.f;
+    if (mine) {
+      float w[3], xr[3];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int p = 3 * lane + a;
+        const float xt = xs[a] + s.dl[p];
+        xr[a] = alpha * xt + (1.f - alpha) * zs[a];
+        xs[a] = alpha * xt + (1.f - alpha) * xs[a];
+        w[a] = xr[a] + ys[a] * inv_rho;
+      }
+      float pv[3];
+      code = project(w[0], w[1], w[2], P.mu, P.fz_min, pv[0], pv[1], pv[2]);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int p = 3 * lane + a;
+        const float zn = pv[a];
+        const float yn = ys[a] + rho * (xr[a] - zn);
+        zs[a] = zn;
+        ys[a] = yn;
+        s.x[p] = xs[a];
+        s.z[p] = zn;
+        const float gp = s.g[p];
+        lrp = fmaxf(lrp, fabsf(xs[a] - zn));
+        lrd = fmaxf(lrd, fabsf(gp + yn));
+        lnp = fmaxf(lnp, fmaxf(fabsf(xs[a]), fabsf(zn)));
+        lnd = fmaxf(lnd, fmaxf(fabsf(gp), fabsf(yn)));
+      }
+      s.code[lane] = code;
+    }
+#ifdef CMPC_TRACE
+    if (b == CMPC_TRACE) {
+      const float trp = wave_max(lrp), trd = wave_max(lrd);
+      if (lane == 0) printf("it %d rho %g rp %g rd %g stable %d\n", it, rho, trp, trd, stable);
+    }
+#endif
+    const bool changed = mine && (code != prev_code);
+    prev_code = code;
+    stable = (__any(changed) != 0) ? 0 : stable + 1;
+    bool do_pol = false;
+    if (stable >= P.polish_stable && !last) {
+      do_pol = true;
+      stable = -P.polish_stable;  // back off before a further attempt
+    }
+    if (adapt || last) {
+      rp = wave_max(lrp); rd = wave_max(lrd); np_ = wave_max(lnp); nd = wave_max(lnd);
+    }
+    if (adapt && !last) {
+      float q = rho * sqrtf((rp / fmaxf(np_, 1e-30f)) / (rd / fmaxf(nd, 1e-30f) + 1e-30f));
+      q = fminf(fmaxf(q, 1e-6f), 1e6f);
+      if (q > 5.f * rho || q < 0.2f * rho) {
+        rho = q;
+        shift = P.sigma + rho;
+        refactor = true;
+      }
+    }
+    if (do_pol) {
+      CMPC_CNT(9, 1);
+      parked = !refactor;  // a pending refactor (rho changed) makes the current inverse stale
+      if (parked) park_store<NC>(park, M);  // restored if the polish fails
+      nact = polish_setup<NC>(s, P, Bg, ntri, tf);
+      shift = P.sigma;
+      refactor = true;
+      in_polish = true;
+      repairs_left = P.polish_repairs;
+    }
+  }
+  if (!polished) {
+    if (n > 0) {
+      const bool conv = rp <= P.eps_abs + P.eps_rel * np_ && rd <= P.eps_abs + P.eps_rel * nd;
+      status = conv ? 2 : -2;
+      if (mine) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) s.z[3 * lane + a] = zs[a];
+      }
+    }
+    gradient<NC>(s, P, n, s.z, s.g);  // E at u = z (the pure rollout when every leg swings)
+  }
+  // ---- outputs: x_{k+1} = e_{k+1} + xref_k, u from the triples (zero on swing legs) ----
+  WSYNC();
+  float* wb = out.w + b * (int64_t)(24 * N);
+  int bad = 0;
+  for (int o = lane; o < NP; o += 64) {
+    const float xv = s.E[o] + xrb[o];
+    bad |= !isfinite(xv);
+    wb[o] = xv;
+    const int k = o / 12, l = (o % 12) / 3, a = o % 3;
+    const int t = s.tri_of[4 * k + l];
+    if (!polished) {  // u = z (ADMM basis)
+      const float uv = (t >= 0) ? s.z[3 * t + a] : 0.f;
+      bad |= !isfinite(uv);
+      wb[NP + o] = uv;
+    } else if (t < 0) {  // swing leg; stance forces are written by the owning lane below
+      wb[NP + o] = 0.f;
+    }
+  }
+  if (polished && mine) {
+    const int kl = s.tri[lane];
+    float* ub = wb + NP + 12 * (kl >> 2) + 3 * (kl & 3);
+    ub[0] = pfx; ub[1] = pfy; ub[2] = pfz;
+    bad |= !(isfinite(pfx) && isfinite(pfy) && isfinite(pfz));
+  }
+  if (__any(bad)) status = -10;
+  if (lane == 0) {
+    out.status[b] = status;
+    out.iters[b] = iters;
+  }
+  CMPC_CNT(11, iters);
+  CMPC_ACC(5, t_inst);
+}
+
+template <int NC>
+__global__ void __launch_bounds__(64, Cfg<NC>::WPE)
+    solve_bin_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list,
+                     const int* __restrict__ count, int* __restrict__ head,
+                     float* __restrict__ work) {
+  using C = Cfg<NC>;
+  __shared__ Smem<NC> s;
+  const int lane = opaque_lane();
+  float* img = work + (size_t)blockIdx.x * C::SLAB;
+  float* park = img + C::IMG;
+  if (lane < 12) {
+    s.Q2[lane] = P.Q2[lane];
+    s.R2[lane] = P.R2[lane];
+  }
+  const int total = *count;
+  for (;;) {
+    int idx = 0;
+    if (lane == 0) idx = atomicAdd(head, 1);
+    idx = __builtin_amdgcn_readfirstlane(idx);
+    if (idx >= total) break;
+    solve_instance<NC>(s, P, (int64_t)list[idx], in, out, img, park);
+  }
+}
+
+__global__ void __launch_bounds__(256) bin_kernel(int N, int64_t B,
+                                                  const uint8_t* __restrict__ contact,
+                                                  int* __restrict__ counts,
+                                                  int* __restrict__ lists, int64_t stride) {
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  int bin = -1;
+  if (b < B) {
+    const uint8_t* c = contact + b * 4 * N;
+    int cnt = 0;
+    if ((N & 3) == 0) {  // 4N bytes = N words
+      const uint32_t* c4 = reinterpret_cast<const uint32_t*>(c);
+      for (int i = 0; i < N; ++i) {
+        const uint32_t v = c4[i];
+        cnt += ((v & 0xffu) != 0) + ((v & 0xff00u) != 0) + ((v & 0xff0000u) != 0) +
+               ((v >> 24) != 0);
+      }
+    } else {
+      for (int i = 0; i < 4 * N; ++i) cnt += c[i] != 0;
+    }
+    const int nf = 3 * cnt;
+    bin = kNumBins - 1;
+    for (int q = 0; q < kNumBins; ++q)
+      if (nf <= kBinCap[q]) { bin = q; break; }
+  }
+  // one atomic per (wave, bin)
+#pragma unroll
+  for (int q = 0; q < kNumBins; ++q) {
+    const unsigned long long m = __ballot(bin == q);
+    if (m == 0) continue;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&counts[q], __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (bin == q) {
+      const int rank = __popcll(m & ((1ull << lane) - 1ull));
+      lists[(int64_t)q * stride + base + rank] = (int)b;
+    }
+  }
+}
+
+}  // namespace cmpc

@@ -36,11 +36,13 @@ def main():
     lib.cmpc_debug_stamps(buf)
     v = np.array(list(buf), dtype=np.float64)
     n = v[10]
-    names = ["condense", "invert", "gradient", "symv", "polish(all)", "instance total"]
+    names = ["condense", "invert", "gradient", "symv", "polish(all)", "instance total",
+             " condense_stage", " gradient mfma"]
     print(f"instances {int(n)}  mean iters {v[11]/n:.2f}  condense_invert/inst {v[8]/n:.2f}  "
           f"polish attempts/inst {v[9]/n:.2f}")
     for i, nm in enumerate(names):
         print(f"  {nm:16s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
+    print(f"  per call: condense {v[0]/v[8]:.0f}  stage {v[6]/v[8]:.0f}  invert {v[1]/v[8]:.0f}  gradient {v[2]/max(v[12],1):.0f} (mfma {v[7]/max(v[12],1):.0f}, x{v[12]/n:.1f})  symv {v[3]/max(v[13],1):.0f} (x{v[13]/n:.1f}) cycles")
     print("  status:", dict(zip(*np.unique(st.cpu().numpy(), return_counts=True))))
 
 
