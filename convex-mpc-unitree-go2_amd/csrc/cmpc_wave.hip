@@ -125,7 +125,7 @@ __device__ __forceinline__ int opaque_lane() {
 // ------------------------------------------------------------------------------------------
 // diagnostic build only (-DCMPC_STAMPS): per-phase s_memtime cycle totals.  Phases: 0 condense
 // (+tile load), 1 invert, 2 gradient, 3 symv, 4 polish (all of it), 5 instance total,
-// 6 condense MFMA+scatter only; counters: 8 condense+invert calls, 9 polish attempts,
+// counters: 8 condense+invert calls, 9 polish attempts,
 // 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls.
 // ------------------------------------------------------------------------------------------
 #ifdef CMPC_STAMPS
@@ -157,8 +157,7 @@ struct Cfg {
   static constexpr int TT = NC / 16;             // 16x16 tile rows
   static constexpr int NTL = TT * (TT + 1) / 2;  // lower-triangle tiles (f4 per lane each)
   static constexpr int THREADS = 64;             // one wave per QP
-  static constexpr int IMG = NTL * 256;          // floats of one tile image
-  static constexpr int SLAB = 2 * IMG;           // per wave: condensation image + park slab
+  static constexpr int SLAB = NTL * 256;         // per wave: park slab of the inverse (floats)
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
   static constexpr int WPE = (4 * NTL <= 150) ? 2 : 1;
 };
@@ -169,17 +168,22 @@ struct Smem {
   alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
   alignas(16) float x[NC];
   alignas(16) float z[NC];
-  alignas(16) float g[NC];
-  alignas(16) float r[NC];
   alignas(16) float v[NC];
-  alignas(16) float dl[NC];
-  alignas(16) float ds[NC];        // unit-diagonal scaling of the sweep
-  alignas(16) float pan[NC * 4];   // sweep panel: 4 pivot columns, row-major [row][4]
+  union {  // buffers that are dead while the matrix is condensed share the G slab
+    struct {
+      alignas(16) float g[NC];
+      alignas(16) float r[NC];
+      alignas(16) float dl[NC];
+      alignas(16) float ds[NC];        // unit-diagonal scaling of the sweep
+      alignas(16) float pan[NC * 4];   // sweep panel: 4 pivot columns, row-major [row][4]
+      float H[kMaxP];                  // h_k = B~_k v_k + d~_k
+      float E[kMaxP];                  // e_{k+1} = x_{k+1} - xref_k
+      float L[kMaxP];                  // lambda_k
+    };
+    alignas(16) float G[NC * 12];      // condensation: G_t column p = A^{t-k_p} b_p
+  };
   float D[kMaxP];                  // d_k  (error-coordinate affine term)
   float Dt[kMaxP];                 // d~_k (d_k + B_k t0_k in the polish basis)
-  float H[kMaxP];                  // h_k = B~_k v_k + d~_k
-  float E[kMaxP];                  // e_{k+1} = x_{k+1} - xref_k
-  float L[kMaxP];                  // lambda_k
   float A[144];
   float Q2[12];                    // KParams copies (indexed at run time -> keep out of kernarg)
   float R2[12];
@@ -194,103 +198,79 @@ struct Smem {
 __device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * (I + 1)) / 2 + J; }
 
 // ------------------------------------------------------------------------------------------
-// condensation (MFMA) -> per-wave tile image (global, lower triangle, accumulator layout)
+// condensation straight into the register tiles (MFMA)
 // ------------------------------------------------------------------------------------------
+// H = sum_t G_t' Q2 G_t + diag(Rt) + shift, where G_t (12 x n) column p is A^{t - k_p} b_p
+// for k_p <= t and 0 otherwise (the prediction matrix row block of step t).  Walking t
+// forward, G_t = A G_{t-1} (three MFMAs per 16-column chunk, K = 12) plus the new columns of
+// step t; each lower tile (I, J) accumulates (Q2 G_t)_I' (G_t)_J with three MFMAs whose
+// accumulator IS the tile (lane (g, c): rows 4g..4g+3, column c).  Tile row I starts to
+// receive terms at the step of its first parameter.
 template <int NC>
-__device__ __forceinline__ f4 load_bcol(const Smem<NC>& s, int p0, int m, int g, int c) {
-  f4 v = {0.f, 0.f, 0.f, 0.f};
-  if (c < m && g < 3) v = *reinterpret_cast<const f4*>(&s.Bt[(p0 + c) * 12 + 4 * g]);
-  return v;
-}
-
-// element (p, q), p >= q, of the symmetric matrix -> image float index
-__device__ __forceinline__ int img_index(int p, int q) {
-  const int r = p & 15, c = q & 15;
-  return tile_index(p >> 4, q >> 4) * 256 + ((r >> 2) * 16 + c) * 4 + (r & 3);
-}
-
-template <int NC>
-__device__ __forceinline__ void condense_image(Smem<NC>& s, const KParams& P,
-                                               float* __restrict__ img) {
-  const int lane = opaque_lane();
-  const int g = lane >> 4, c = lane & 15;
-  const int N = P.N;
-  float Ar[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = 4 * g + q;
-    Ar[q] = (row < 12 && c < 12) ? s.A[row * 12 + c] : 0.f;
-  }
-  f4 S;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = 4 * g + q;
-    S[q] = (row < 12 && row == c) ? s.Q2[row] : 0.f;
-  }
-  for (int j = N - 1; j >= 0; --j) {
-    if (j < N - 1) {  // S_j = Q2 + A' (S_{j+1} A)
-      f4 T1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) T1 = mfma4(S[q], Ar[q], T1);
-      f4 Sn = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Sn = mfma4(Ar[q], T1[q], Sn);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = 4 * g + q;
-        if (row < 12 && row == c) Sn[q] += s.Q2[row];
-      }
-      S = Sn;
-    }
-    const int pj0 = s.off[j], mj = s.off[j + 1] - pj0;
-    if (mj == 0) continue;
-    const f4 bj = load_bcol(s, pj0, mj, g, c);
-    f4 W = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) W = mfma4(S[q], bj[q], W);
-    for (int i = j; i >= 0; --i) {
-      if (i < j) {  // W <- A' W
-        f4 Wn = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) Wn = mfma4(Ar[q], W[q], Wn);
-        W = Wn;
-      }
-      const int pi0 = s.off[i], mi = s.off[i + 1] - pi0;
-      if (mi == 0) continue;
-      const f4 bi = load_bcol(s, pi0, mi, g, c);
-      f4 Hb = {0.f, 0.f, 0.f, 0.f};  // Hb[q] = H[pi0 + 4g+q][pj0 + c]
-#pragma unroll
-      for (int q = 0; q < 4; ++q) Hb = mfma4(bi[q], W[q], Hb);
-      const int p = pj0 + c;  // lower triangle: row p >= column qc
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int qq = 4 * g + q, qc = pi0 + qq;
-        if (qq < mi && c < mj && (i != j || c >= qq)) {
-          img[img_index(p, qc)] = Hb[q];
-          if ((p >> 4) == (qc >> 4) && p != qc) img[img_index(qc, p)] = Hb[q];
-        }
-      }
-    }
-  }
-}
-
-// register tiles <- image, + diag(Rt) + shift, identity on padding
-template <int NC>
-__device__ __forceinline__ void load_tiles(f4 (&M)[Cfg<NC>::NTL], const Smem<NC>& s,
-                                           const float* __restrict__ img, int n, float shift) {
+__device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
+                                               f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
   using C = Cfg<NC>;
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
+  const int N = P.N;
   const int TA = (n + 15) >> 4;
-  // own stores of this wave are in L2; drop any stale L1 copy of the image before reading
-  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < C::NTL; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int e = lane; e < NC * 12; e += 64) s.G[e] = 0.f;
+  float aA[3], q2[3];  // A[c][4st + g] (A operand of A G), Q2[4st + g]
+#pragma unroll
+  for (int st = 0; st < 3; ++st) {
+    aA[st] = (c < 12) ? s.A[c * 12 + 4 * st + g] : 0.f;
+    q2[st] = s.Q2[4 * st + g];
+  }
+  int kI[C::TT];  // first step of tile row I (N: no parameters)
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) kI[I] = (16 * I < n) ? s.par[16 * I] : N;
+  for (int t = 0; t < N; ++t) {
+    WSYNC();
+    if (t > 0) {  // G_t = A G_{t-1} on the chunks that already hold columns
+#pragma unroll
+      for (int ch = 0; ch < C::TT; ++ch) {
+        if (kI[ch] >= t) continue;  // uniform
+        const float* col = &s.G[(16 * ch + c) * 12];
+        f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) d = mfma4(aA[st], col[4 * st + g], d);
+        if (g < 3) *reinterpret_cast<f4*>(&s.G[(16 * ch + c) * 12 + 4 * g]) = d;
+      }
+      WSYNC();
+    }
+    const int p0 = s.off[t], m = s.off[t + 1] - p0;  // new columns b_p of step t
+    for (int e = lane; e < 12 * m; e += 64) s.G[p0 * 12 + e] = s.Bt[p0 * 12 + e];
+    WSYNC();
+    float b[C::TT][3];
+#pragma unroll
+    for (int J = 0; J < C::TT; ++J) {
+#pragma unroll
+      for (int st = 0; st < 3; ++st)
+        b[J][st] = (kI[J] <= t) ? s.G[(16 * J + c) * 12 + 4 * st + g] : 0.f;
+    }
+#pragma unroll
+    for (int I = 0; I < C::TT; ++I) {
+      if (kI[I] > t) continue;  // uniform: row block I has no column yet
+      float a[3];
+#pragma unroll
+      for (int st = 0; st < 3; ++st) a[st] = q2[st] * b[I][st];
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        f4 acc = M[tile_index(I, J)];
+#pragma unroll
+        for (int st = 0; st < 3; ++st) acc = mfma4(a[st], b[J][st], acc);
+        M[tile_index(I, J)] = acc;
+      }
+    }
+  }
+  // + diag(Rt) + shift, identity on padding
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) {
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
-      const int t = tile_index(I, J);
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (I < TA) v = *reinterpret_cast<const f4*>(&img[t * 256 + lane * 4]);
+      f4 v = M[tile_index(I, J)];
       const int col = 16 * J + c;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -298,9 +278,11 @@ __device__ __forceinline__ void load_tiles(f4 (&M)[Cfg<NC>::NTL], const Smem<NC>
         if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
         else if (row == col) v[q] += s.Rt[row] + shift;
       }
-      M[t] = v;
+      M[tile_index(I, J)] = v;
     }
   }
+  (void)TA;
+  WSYNC();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -781,7 +763,6 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 template <int NC>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
-                                               float* __restrict__ img,
                                                float* __restrict__ park) {
   using C = Cfg<NC>;
   f4 M[C::NTL];
@@ -842,9 +823,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     if (refactor) {  // the only condense + invert call site
       CMPC_CNT(8, 1);
       CMPC_T0(t_c);
-      condense_image<NC>(s, P, img);
-      CMPC_ACC(6, t_c);
-      load_tiles<NC>(M, s, img, nact, shift);
+      condense_tiles<NC>(s, P, M, nact, shift);
       CMPC_ACC(0, t_c);
       CMPC_T0(t_i);
       invert_tiles<NC>(s, M, nact);
@@ -1037,8 +1016,7 @@ __global__ void __launch_bounds__(64, Cfg<NC>::WPE)
   using C = Cfg<NC>;
   __shared__ Smem<NC> s;
   const int lane = opaque_lane();
-  float* img = work + (size_t)blockIdx.x * C::SLAB;
-  float* park = img + C::IMG;
+  float* park = work + (size_t)blockIdx.x * C::SLAB;
   if (lane < 12) {
     s.Q2[lane] = P.Q2[lane];
     s.R2[lane] = P.R2[lane];
@@ -1049,7 +1027,7 @@ __global__ void __launch_bounds__(64, Cfg<NC>::WPE)
     if (lane == 0) idx = atomicAdd(head, 1);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= total) break;
-    solve_instance<NC>(s, P, (int64_t)list[idx], in, out, img, park);
+    solve_instance<NC>(s, P, (int64_t)list[idx], in, out, park);
   }
 }
 

@@ -84,9 +84,9 @@ __global__ void __launch_bounds__(64) k_condense(KParams P, const float* Ad, con
   gradient<NC>(s, P, n, s.v, s.g);
   for (int p = lane; p < n; p += 64) gout[p] = s.g[p];
   for (int o = lane; o < 12 * N; o += 64) Eout[o] = s.E[o];
-  condense_image<NC>(s, P, img);
   f4 M[C::NTL];
-  load_tiles<NC>(M, s, img, n, 0.f);
+  condense_tiles<NC>(s, P, M, n, 0.f);
+  (void)img;
 #pragma unroll
   for (int I = 0; I < C::TT; ++I)
 #pragma unroll
@@ -112,9 +112,9 @@ extern "C" int wave_condense(const float* Q2, const float* R2, int N, const floa
   uint8_t* dc;
   int* dn;
   (void)hipMalloc(&dA, 144 * 4); (void)hipMalloc(&dB, N * 144 * 4);
-  (void)hipMalloc(&dc, 4 * N); (void)hipMalloc(&dimg, Cfg<128>::IMG * 4);
+  (void)hipMalloc(&dc, 4 * N); (void)hipMalloc(&dimg, Cfg<128>::SLAB * 4);
   (void)hipMalloc(&dout, 128 * 128 * 4); (void)hipMalloc(&dn, 4);
-  (void)hipMemset(dimg, 0, Cfg<128>::IMG * 4);
+  (void)hipMemset(dimg, 0, Cfg<128>::SLAB * 4);
   float *dd, *dv, *dg, *dE;
   (void)hipMalloc(&dd, 192 * 4); (void)hipMalloc(&dv, 192 * 4);
   (void)hipMalloc(&dg, 192 * 4); (void)hipMalloc(&dE, 192 * 4);
