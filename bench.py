@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--traffic-json", type=str, default=str(REPO / "profiles" / "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
     ap.add_argument("--latency-batch", type=int, default=256)
+    ap.add_argument("--lib", type=str, default=None,
+                    help="alternative build of libcmpc.so (A/B experiments)")
     return ap.parse_args()
 
 
@@ -71,6 +73,9 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
     torch.cuda.set_device(dev)
 
+    if args.lib:
+        from cmpc import _lib
+        _lib._lib = _lib.load(args.lib)
     from cmpc import Plan, SolverParams, to_device_batch, synth
 
     B = args.batch

@@ -37,6 +37,10 @@
 
 namespace cmpc {
 
+#ifndef CMPC_WPE_OVERRIDE
+#define CMPC_WPE_OVERRIDE ((4 * NTL <= 150) ? 2 : 1)
+#endif
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------
@@ -159,7 +163,7 @@ struct Cfg {
   static constexpr int THREADS = 64;             // one wave per QP
   static constexpr int SLAB = NTL * 256;         // per wave: park slab of the inverse (floats)
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
-  static constexpr int WPE = (4 * NTL <= 150) ? 2 : 1;
+  static constexpr int WPE = CMPC_WPE_OVERRIDE;
 };
 
 template <int NC>
@@ -317,71 +321,67 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
     }
   }
   const int ng = (n + 3) >> 2;
+  const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
   for (int st = 0; st < ng; ++st) {
     const int k0 = 4 * st, K = k0 >> 4, c0 = k0 & 15, gp = c0 >> 2;
-    // publish the 4 pivot columns (current values) as panel rows [row][0..3]
+    const int pc = c - c0;
+    const bool colw = pc >= 0 && pc < 4, roww = g == gp;
+    // publish the 4 pivot columns (current values) as panel rows [row][0..3]: column part from
+    // tiles (I >= K, K), row part (transposed) from tiles (K, J < K); every panel row is
+    // rewritten each step, padding rows included.  One uniform branch selects K's tiles.
 #pragma unroll
-    for (int I = 0; I < C::TT; ++I) {
+    for (int KK = 0; KK < C::TT; ++KK) {
+      if (KK != K) continue;
+      if (colw) {
 #pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        const f4 m = M[tile_index(I, J)];
-        if (J == K && I < TA) {  // column part: rows 16I + 4g + q, panel column c - c0
-          const int pc = c - c0;
-          if (pc >= 0 && pc < 4) {
+        for (int I = KK; I < C::TT; ++I) {
+          f4 m = M[tile_index(I, KK)];
+          if (I == KK) {  // P^ = P - I on the 4 pivot rows
 #pragma unroll
-            for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
+            for (int q = 0; q < 4; ++q) m[q] -= (4 * g + q == c) ? 1.f : 0.f;
           }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
         }
-        if (I == K && J < K) {  // row part (transposed): rows k0..k0+3 of tile (K, J)
-          if (g == gp) *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = m;
-        }
+      }
+      if (roww) {
+#pragma unroll
+        for (int J = 0; J < KK; ++J)
+          *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(KK, J)];
       }
     }
     WSYNC();
     // D = L diag(dl) L' (unit lower L), so P^ D^-1 P^' = Y diag(1/dl) Y' with Y = P^ L^-T: the
     // columns of Y are the pivot columns as the scalar sweep would see them (each already
     // eliminated by the earlier pivots of the step), which keeps the scalar sweep's accuracy.
-    float Dm[16];
+    float Dm[16];  // the panel holds P^ = P - I: add the identity back for D
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const f4 rrow = *reinterpret_cast<const f4*>(&s.pan[(k0 + i) * 4]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j];
+      for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j] + ((i == j) ? 1.f : 0.f);
     }
-    const float d0 = Dm[0];
-    const float i0 = __builtin_amdgcn_rcpf(d0);
+    const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
     const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
-    const float d1 = Dm[5] - l10 * Dm[4];
-    const float i1 = __builtin_amdgcn_rcpf(d1);
-    const float l21 = (Dm[9] - l20 * Dm[4]) * i1;
-    const float l31 = (Dm[13] - l30 * Dm[4]) * i1;
-    const float d2 = Dm[10] - l20 * Dm[8] - l21 * (Dm[9] - l20 * Dm[4]);
-    const float i2 = __builtin_amdgcn_rcpf(d2);
-    const float l32 = (Dm[14] - l30 * Dm[8] - l31 * (Dm[9] - l20 * Dm[4])) * i2;
-    const float d3 = Dm[15] - l30 * Dm[12] - l31 * (Dm[13] - l30 * Dm[4]) -
-                     l32 * (Dm[14] - l30 * Dm[8] - l31 * (Dm[9] - l20 * Dm[4]));
-    const float i3 = __builtin_amdgcn_rcpf(d3);
-    const float ig = (g == 0) ? i0 : (g == 1) ? i1 : (g == 2) ? i2 : i3;
+    const float i1 = __builtin_amdgcn_rcpf(Dm[5] - l10 * Dm[4]);
+    const float u21 = Dm[9] - l20 * Dm[4], u31 = Dm[13] - l30 * Dm[4];
+    const float l21 = u21 * i1, l31 = u31 * i1;
+    const float i2 = __builtin_amdgcn_rcpf(Dm[10] - l20 * Dm[8] - l21 * u21);
+    const float u32 = Dm[14] - l30 * Dm[8] - l31 * u21;
+    const float l32 = u32 * i2;
+    const float i3 = __builtin_amdgcn_rcpf(Dm[15] - l30 * Dm[12] - l31 * u31 - l32 * u32);
+    const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
     float a[C::TT], b[C::TT];
 #pragma unroll
     for (int I = 0; I < C::TT; ++I) {
-      if (I < TA) {
-        const int row = 16 * I + c;
-        const f4 pr = *reinterpret_cast<const f4*>(&s.pan[row * 4]);
-        float ph[4];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) ph[m] = pr[m] - ((row == k0 + m) ? 1.f : 0.f);
-        const float y0 = ph[0];
-        const float y1 = ph[1] - l10 * y0;
-        const float y2 = ph[2] - l20 * y0 - l21 * y1;
-        const float y3 = ph[3] - l30 * y0 - l31 * y1 - l32 * y2;
-        const float yg = (g == 0) ? y0 : (g == 1) ? y1 : (g == 2) ? y2 : y3;
-        a[I] = -yg;
-        b[I] = yg * ig;
-      } else {
-        a[I] = 0.f;
-        b[I] = 0.f;
-      }
+      const f4 ph = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
+      const float y0 = ph[0];
+      const float y1 = ph[1] - l10 * y0;
+      const float y2 = ph[2] - l20 * y0 - l21 * y1;
+      const float y3 = ph[3] - l30 * y0 - l31 * y1 - l32 * y2;
+      const float yg = g3 ? y3 : g2 ? y2 : g1 ? y1 : y0;
+      a[I] = -yg;
+      b[I] = yg * ig;
     }
 #pragma unroll
     for (int I = 0; I < C::TT; ++I) {
@@ -393,13 +393,11 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
       }
     }
 #pragma unroll
-    for (int I = 0; I < C::TT; ++I) {
-      if (I == K) {
-        f4& m = M[tile_index(I, I)];
+    for (int KK = 0; KK < C::TT; ++KK) {  // -2 on the 4 pivot diagonals
+      if (KK != K) continue;
+      f4& m = M[tile_index(KK, KK)];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (g == gp && c == c0 + q) m[q] -= 2.f;
-      }
+      for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
     }
   }
   // M holds -(scaled inverse): undo sign and scaling
