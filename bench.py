@@ -34,6 +34,27 @@ BYTES_IN = 576 + 9216 + 48 + 48 + 768 + 64      # Ad, Bd, gd, x0, xref, contact 
 BYTES_OUT = 1536 + 4 + 4                         # w, status, iters
 BYTES_PER_SOLVE = BYTES_IN + BYTES_OUT           # 12,264
 HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s spec
+F32_MATRIX_PEAK_TFS = 157.3                      # MI355X_MICROARCH.md: dense f32 MFMA peak
+POLISH_REFINE = 4                                # SolverParams.polish_refine (default)
+
+
+def algorithmic_flops(contact, iters, N=16):
+    """Algorithmic FP32 work per instance of the path's algorithm (DESIGN.md "Roofline"):
+    one ADMM and one polish factorisation at the instance's free-force count n (condensation
+    sum_t 12 m_t^2 + 288 m_{t-1} with m_t = free forces of steps <= t, sweep inverse n^3),
+    `iters` ADMM iterations and POLISH_REFINE refinements of symv (2 n^2) + gradient
+    (576 N + 48 n).  Counts only the accepted path (no rho refactors, repairs or padding)."""
+    st = (contact != 0).reshape(contact.shape[0], 4, -1)           # (B, 4, N)
+    per_step = 3 * st.sum(1).astype(np.float64)                     # free forces per step
+    m = np.cumsum(per_step, axis=1)                                 # m_t
+    n = m[:, -1]
+    m_prev = np.concatenate([np.zeros((m.shape[0], 1)), m[:, :-1]], axis=1)
+    cond = (12.0 * m ** 2 + 288.0 * m_prev).sum(1)
+    inv = n ** 3
+    symv = 2.0 * n ** 2
+    grad = 576.0 * N + 48.0 * n
+    it = iters.astype(np.float64)
+    return 2.0 * (cond + inv) + it * (symv + grad) + POLISH_REFINE * symv + (POLISH_REFINE + 1) * grad
 
 
 def parse():
@@ -133,6 +154,9 @@ def main():
     n_in_bin = int(np.sum(bins == q))
     avg_ms = ms_bins[q] / max(calls[q], 1)
     achieved_gbs = BYTES_PER_SOLVE * n_in_bin / (avg_ms * 1e-3) / 1e9
+    flops = algorithmic_flops(batch["contact"], iters)
+    fl_bin = float(flops[bins == q].sum())
+    achieved_tfs = fl_bin / (avg_ms * 1e-3) / 1e12
     traffic = None
     if args.traffic_json and Path(args.traffic_json).exists():
         tj = json.loads(Path(args.traffic_json).read_text())
@@ -178,10 +202,17 @@ def main():
                          "kernel": f"solve_bin_kernel<{[96, 128, 160, 192][q]}>",
                          "kernel_avg_ms": avg_ms, "solves_per_launch": n_in_bin,
                          "bytes_per_solve": BYTES_PER_SOLVE},
+            "roofline_compute": {"bound": "mfma", "achieved": achieved_tfs,
+                                 "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
+                                 "frac": achieved_tfs / F32_MATRIX_PEAK_TFS,
+                                 "flops_per_solve": fl_bin / max(n_in_bin, 1)},
             "cpu_baseline": cpu,
             "solved_frac": solved_frac,
             "iters_mean": float(np.mean(iters)),
             "latency_ms_b256": lat_ms,
+            "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
+                                for i, c in enumerate((96, 128, 160, 192))},
+            "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

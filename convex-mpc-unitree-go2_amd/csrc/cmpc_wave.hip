@@ -52,11 +52,18 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+
+// wave-uniform copy of a value the compiler cannot prove uniform (keeps branches scalar)
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // v[l] and v[l ^ 32] (resp. v[l ^ 16]) without address registers (gfx950 permlane swaps):
 // after the swap the two results hold the lane's own value and its partner's in some order
+#ifdef CMPC_SHFL_PAIRS
+__device__ __forceinline__ void pair32(float v, float& a, float& b) { a = v; b = __shfl_xor(v, 32, 64); }
+__device__ __forceinline__ void pair16(float v, float& a, float& b) { a = v; b = __shfl_xor(v, 16, 64); }
+#else
 __device__ __forceinline__ void pair32(float v, float& a, float& b) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
   a = __int_as_float(r[0]);
@@ -67,6 +74,7 @@ __device__ __forceinline__ void pair16(float v, float& a, float& b) {
   a = __int_as_float(r[0]);
   b = __int_as_float(r[1]);
 }
+#endif
 
 // max over the wave, result in every lane
 __device__ __forceinline__ float wave_max(float v) {
@@ -129,6 +137,7 @@ __device__ __forceinline__ int opaque_lane() {
 // ------------------------------------------------------------------------------------------
 // diagnostic build only (-DCMPC_STAMPS): per-phase s_memtime cycle totals.  Phases: 0 condense
 // (+tile load), 1 invert, 2 gradient, 3 symv, 4 polish (all of it), 5 instance total,
+// 6 setup, 7 ADMM iteration outside gradient/symv, 14 polish setup, 15 output (+final gradient);
 // counters: 8 condense+invert calls, 9 polish attempts,
 // 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls.
 // ------------------------------------------------------------------------------------------
@@ -172,6 +181,7 @@ struct Smem {
   alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
   alignas(16) float x[NC];
   alignas(16) float z[NC];
+  alignas(16) float y[NC];         // ADMM dual (x, z, y of triple t at 3t .. 3t+2)
   alignas(16) float v[NC];
   union {  // buffers that are dead while the matrix is condensed share the G slab
     struct {
@@ -197,6 +207,8 @@ struct Smem {
   int tri_of[kMaxTri];             // 4k + leg -> triple index or -1
   int tcnt[kMaxTri];               // polish: params of triple t / repaired face code
   int code[kMaxTri];               // face code of triple t
+  int pcode[kMaxTri];              // face code of the previous ADMM iteration
+  int fpk[kMaxTri];                // polish: params of triple t, px | py << 8 | pz << 16 (255 none)
 };
 
 __device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * (I + 1)) / 2 + J; }
@@ -217,6 +229,7 @@ __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
   const int N = P.N;
+  n = uniform(n);
   const int TA = (n + 15) >> 4;
 #pragma unroll
   for (int t = 0; t < C::NTL; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
@@ -297,6 +310,7 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
   using C = Cfg<NC>;
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
+  n = uniform(n);
   const int TA = (n + 15) >> 4;
   // unit-diagonal scaling (padding: 1)
 #pragma unroll
@@ -415,7 +429,7 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
 }
 
 // out = M in over the first n params (M in register tiles, symmetric, lower triangle stored);
-// `in` must be zero for n <= p < NC
+// `in` is read (and treated as zero) beyond n, out is zero there
 template <int NC>
 __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], int n,
                                      const float* in, float* out) {
@@ -423,12 +437,13 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
   CMPC_T0(t_sv);
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
+  n = uniform(n);
   const int TA = (n + 15) >> 4;
   WSYNC();
   float xc[C::TT], cacc[C::TT];
 #pragma unroll
   for (int J = 0; J < C::TT; ++J) {
-    xc[J] = in[16 * J + c];
+    xc[J] = (16 * J + c < n) ? in[16 * J + c] : 0.f;
     cacc[J] = 0.f;
   }
 #pragma unroll
@@ -437,7 +452,9 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
       if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = f4{0.f, 0.f, 0.f, 0.f};
       continue;
     }
-    const f4 xr = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
+    f4 xr = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xr[q] = (16 * I + 4 * g + q < n) ? xr[q] : 0.f;
     f4 racc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
@@ -471,56 +488,98 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
 
 // Gradient of sum_k e_{k+1}'(Q2/2)e_{k+1} + v'(Rt/2)v in the current param basis
 // (e by the error-coordinate rollout).  Leaves E (e_{k+1}) and L (lambda_k) in LDS.
+//
+// Both recursions run as log-depth scans on the matrix cores, the 12 x N state trajectory
+// held as ONE accumulator tile (lane (g, c): states 4g..4g+3 of step c):
+//   forward  e_{k+1} = sum_j A^{k-j} h_j :   E <- E + A^d shift_d(E),      d = 1, 2, 4, 8
+//   adjoint  lambda_k = sum_j (A')^{j-k} Q2 e_{j+1} : L <- L + (A')^d shift_-d(L)
+// (Hillis-Steele; the step shift is a DPP row shift, the product four MFMAs whose accumulator
+// is the trajectory itself).  A^d and (A')^d come from repeated squaring in the same layout.
 template <int NC>
 __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, const float* vin,
                                          float* gout) {
   CMPC_T0(t_gr);
   const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
   const int N = P.N;
-  const int NP = 12 * N;
+  n = uniform(n);
   WSYNC();
-  for (int o = lane; o < NP; o += 64) {  // h_k = B~_k v_k + d~_k
-    const int k = o / 12, r = o % 12;
-    float acc = s.Dt[o];
-    for (int p = s.off[k]; p < s.off[k + 1]; ++p) acc = fmaf(s.Bt[p * 12 + r], vin[p], acc);
-    s.H[o] = acc;
-  }
-  WSYNC();
-  {  // sequential recursions (lanes 0..11 carry the state)
-    const int i = lane % 12;
-    float Arow[12], Acol[12];
+  // h_k = B~_k v_k + d~_k for states 4g..4g+3 of step c
+  f4 Et = {0.f, 0.f, 0.f, 0.f};
+  if (c < N && g < 3) {
+    Et = *reinterpret_cast<const f4*>(&s.Dt[12 * c + 4 * g]);
+    const int p1 = s.off[c + 1];
+    for (int p = s.off[c]; p < p1; ++p) {
+      const f4 bt = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+      const float vp = vin[p];
 #pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      Arow[j] = s.A[i * 12 + j];
-      Acol[j] = s.A[j * 12 + i];
-    }
-    float e = 0.f;
-    for (int k = 0; k < N; ++k) {  // e_{k+1} = A e_k + h_k
-      float a0 = s.H[12 * k + i], a1 = 0.f, a2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 12; j += 3) {
-        a0 = fmaf(Arow[j], readlane_f(e, j), a0);
-        a1 = fmaf(Arow[j + 1], readlane_f(e, j + 1), a1);
-        a2 = fmaf(Arow[j + 2], readlane_f(e, j + 2), a2);
-      }
-      e = a0 + (a1 + a2);
-      if (lane < 12) s.E[12 * k + i] = e;
-    }
-    float lam = 0.f;
-    const float q2 = s.Q2[i];
-    WSYNC();
-    for (int k = N - 1; k >= 0; --k) {  // lambda_k = Q2 e_{k+1} + A' lambda_{k+1}
-      float a0 = q2 * s.E[12 * k + i], a1 = 0.f, a2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < 12; j += 3) {
-        a0 = fmaf(Acol[j], readlane_f(lam, j), a0);
-        a1 = fmaf(Acol[j + 1], readlane_f(lam, j + 1), a1);
-        a2 = fmaf(Acol[j + 2], readlane_f(lam, j + 2), a2);
-      }
-      lam = a0 + (a1 + a2);
-      if (lane < 12) s.L[12 * k + i] = lam;
+      for (int q = 0; q < 4; ++q) Et[q] = fmaf(bt[q], vp, Et[q]);
     }
   }
+  // powers: Pd = A^d and Td = (A')^d in accumulator layout (Pd[q] = A^d[4g+q][c])
+  f4 Pd, Td;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * g + q;
+    Pd[q] = (r < 12 && c < 12) ? s.A[r * 12 + c] : 0.f;
+    Td[q] = (r < 12 && c < 12) ? s.A[c * 12 + r] : 0.f;
+  }
+  f4 pw[4], tw[4];  // d = 1, 2, 4, 8
+  pw[0] = Pd;
+  tw[0] = Td;
+#pragma unroll
+  for (int l = 1; l < 4; ++l) {
+    f4 pn = {0.f, 0.f, 0.f, 0.f}, tn = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pn = mfma4(tw[l - 1][q], pw[l - 1][q], pn);  // A^2d  = A^d A^d   (A operand = (A^d)')
+      tn = mfma4(pw[l - 1][q], tw[l - 1][q], tn);  // A'^2d = A'^d A'^d
+    }
+    pw[l] = pn;
+    tw[l] = tn;
+  }
+  // forward scan: E[:, k] += A^d E[:, k - d]  (A operand = (A^d)' = tw)
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    if ((1 << l) >= N) break;  // uniform
+    f4 sh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      switch (l) {
+        case 0: sh[q] = dpp<0x111>(Et[q]); break;  // row_shr:1
+        case 1: sh[q] = dpp<0x112>(Et[q]); break;  // row_shr:2
+        case 2: sh[q] = dpp<0x114>(Et[q]); break;  // row_shr:4
+        default: sh[q] = dpp<0x118>(Et[q]); break; // row_shr:8
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Et = mfma4(tw[l][q], sh[q], Et);
+  }
+  if (c < N && g < 3) *reinterpret_cast<f4*>(&s.E[12 * c + 4 * g]) = Et;
+  // adjoint: L0 = Q2 e_{k+1} (zero past the horizon), L[:, k] += (A')^d L[:, k + d]
+  f4 Lt;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * g + q;
+    Lt[q] = (c < N && r < 12) ? s.Q2[r] * Et[q] : 0.f;
+  }
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    if ((1 << l) >= N) break;
+    f4 sh;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      switch (l) {
+        case 0: sh[q] = dpp<0x101>(Lt[q]); break;  // row_shl:1
+        case 1: sh[q] = dpp<0x102>(Lt[q]); break;  // row_shl:2
+        case 2: sh[q] = dpp<0x104>(Lt[q]); break;  // row_shl:4
+        default: sh[q] = dpp<0x108>(Lt[q]); break; // row_shl:8
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Lt = mfma4(pw[l][q], sh[q], Lt);  // A operand = A^d = ((A')^d)'
+  }
+  if (c < N && g < 3) *reinterpret_cast<f4*>(&s.L[12 * c + 4 * g]) = Lt;
   WSYNC();
   for (int p = lane; p < n; p += 64) {  // g = B~' lambda + Rt v
     const int k = s.par[p];
@@ -566,12 +625,20 @@ __device__ __forceinline__ void build_admm_basis(Smem<NC>& s, const KParams& P,
   const int N = P.N;
   const int n = 3 * ntri;
   WSYNC();
-  for (int e = lane; e < n * 12; e += 64) {
-    const int p = e / 12, r = e % 12;
-    const int t = p / 3, a = p % 3;
-    const int kl = s.tri[t];
-    const int k = kl >> 2, leg = kl & 3;
-    s.Bt[e] = Bg[(k * 12 + r) * 12 + 3 * leg + a];
+  if (lane < ntri) {  // lane t copies the 12x3 block of its triple (all loads in flight at once)
+    const int kl = s.tri[lane];
+    const float* src = Bg + (kl >> 2) * 144 + 3 * (kl & 3);
+    float bv[36];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) bv[3 * r + a] = src[r * 12 + a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+      for (int r = 0; r < 12; ++r) s.Bt[(3 * lane + a) * 12 + r] = bv[3 * r + a];
+    }
   }
   for (int p = lane; p < NC; p += 64) {
     if (p < n) {
@@ -596,61 +663,70 @@ __device__ __forceinline__ void build_admm_basis(Smem<NC>& s, const KParams& P,
 }
 
 // Polish setup: the reduced basis of the faces in s.code (lane t owns triple t),
-// u = T v + t0 with t0 = locked components, v initialised from z.  Returns nr.
-struct TripleFaces {
-  int k, leg, sx, sy, px, py, pz;
-  bool zl, owns;
-};
-
+// u = T v + t0 with t0 = locked components, v initialised from z.  Returns nr; the param
+// indices of each triple are left packed in s.fpk for the KKT check.
 template <int NC>
 __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
-                                            const float* __restrict__ Bg, int ntri,
-                                            TripleFaces& tf) {
+                                            const float* __restrict__ Bg, int ntri) {
   const int lane = opaque_lane();
   const int N = P.N;
   const float mu = P.mu, fzmin = P.fz_min;
-  tf = TripleFaces{0, 0, 0, 0, -1, -1, -1, false, false};
   WSYNC();
-  tf.owns = lane < ntri;
-  const int code = tf.owns ? s.code[lane] : 0;
-  const int kl = tf.owns ? s.tri[lane] : 0;
+  const bool owns = lane < ntri;
+  const int code = owns ? s.code[lane] : 0;
+  const int kl = owns ? s.tri[lane] : 0;
   const int k = kl >> 2, leg = kl & 3;
   const int sx = (code & 2) ? 1 : ((code & 4) ? -1 : 0);
   const int sy = (code & 8) ? 1 : ((code & 16) ? -1 : 0);
   const bool zl = (code & 1) != 0;
-  tf.k = k; tf.leg = leg; tf.sx = sx; tf.sy = sy; tf.zl = zl;
-  const int cnt = tf.owns ? ((sx == 0) + (sy == 0) + (!zl)) : 0;
+  const int cnt = owns ? ((sx == 0) + (sy == 0) + (!zl)) : 0;
   const int base = wave_excl_scan4(cnt);
   const int nr = wave_total4(cnt);
-  const float* Bk = Bg + k * 144;
-  if (tf.owns) {
+  if (owns) {
+    float bx[12], by[12], bz[12];  // columns fx, fy, fz of B_k for this leg (loads in flight together)
+    {
+      const float* src = Bg + k * 144 + 3 * leg;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) {
+        bx[r] = src[r * 12];
+        by[r] = src[r * 12 + 1];
+        bz[r] = src[r * 12 + 2];
+      }
+    }
     s.tcnt[lane] = cnt;
     int p = base;
+    int px = 255, py = 255, pz = 255;
     if (sx == 0) {
-      tf.px = p++;
-      for (int r = 0; r < 12; ++r) s.Bt[tf.px * 12 + r] = Bk[r * 12 + 3 * leg];
-      s.Rt[tf.px] = s.R2[3 * leg];
-      s.par[tf.px] = k;
-      s.v[tf.px] = s.z[3 * lane];
+      px = p++;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) s.Bt[px * 12 + r] = bx[r];
+      s.Rt[px] = s.R2[3 * leg];
+      s.par[px] = k;
+      s.v[px] = s.z[3 * lane];
     }
     if (sy == 0) {
-      tf.py = p++;
-      for (int r = 0; r < 12; ++r) s.Bt[tf.py * 12 + r] = Bk[r * 12 + 3 * leg + 1];
-      s.Rt[tf.py] = s.R2[3 * leg + 1];
-      s.par[tf.py] = k;
-      s.v[tf.py] = s.z[3 * lane + 1];
+      py = p++;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) s.Bt[py * 12 + r] = by[r];
+      s.Rt[py] = s.R2[3 * leg + 1];
+      s.par[py] = k;
+      s.v[py] = s.z[3 * lane + 1];
     }
     if (!zl) {
-      tf.pz = p++;
+      pz = p++;
       const float cx = sx * mu, cy = sy * mu;
-      for (int r = 0; r < 12; ++r)
-        s.Bt[tf.pz * 12 + r] = Bk[r * 12 + 3 * leg + 2] + cx * Bk[r * 12 + 3 * leg] +
-                               cy * Bk[r * 12 + 3 * leg + 1];
-      s.Rt[tf.pz] = s.R2[3 * leg + 2] + mu * mu * ((sx != 0 ? s.R2[3 * leg] : 0.f) +
-                                                   (sy != 0 ? s.R2[3 * leg + 1] : 0.f));
-      s.par[tf.pz] = k;
-      s.v[tf.pz] = s.z[3 * lane + 2];
+#pragma unroll
+      for (int r = 0; r < 12; ++r) s.Bt[pz * 12 + r] = bz[r] + cx * bx[r] + cy * by[r];
+      s.Rt[pz] = s.R2[3 * leg + 2] + mu * mu * ((sx != 0 ? s.R2[3 * leg] : 0.f) +
+                                                (sy != 0 ? s.R2[3 * leg + 1] : 0.f));
+      s.par[pz] = k;
+      s.v[pz] = s.z[3 * lane + 2];
+    } else {  // fz locked at fz_min: the triple's constant force t0 enters d~ through B_k t0
+      const float tx = sx * mu * fzmin, ty = sy * mu * fzmin;
+#pragma unroll
+      for (int r = 0; r < 12; ++r) s.G[lane * 12 + r] = fmaf(bz[r], fzmin, fmaf(by[r], ty, bx[r] * tx));
     }
+    s.fpk[lane] = px | (py << 8) | (pz << 16);
   }
   WSYNC();
   for (int kk = lane; kk <= N; kk += 64) {
@@ -658,54 +734,56 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
     for (int t = 0; t < ntri; ++t) c += ((s.tri[t] >> 2) < kk) ? s.tcnt[t] : 0;
     s.off[kk] = c;
   }
-  for (int o = lane; o < 12 * N; o += 64) {  // d~ = d + B t0 (fz locked at fz_min)
+  for (int o = lane; o < 12 * N; o += 64) {  // d~ = d + B t0 (LDS only)
     const int kk = o / 12, r = o % 12;
     float acc = s.D[o];
+#pragma unroll
     for (int l = 0; l < 4; ++l) {
       const int t = s.tri_of[4 * kk + l];
-      if (t < 0) continue;
-      const int c = s.code[t];
-      if (!(c & 1)) continue;
-      const float tx = (c & 2) ? mu * fzmin : ((c & 4) ? -mu * fzmin : 0.f);
-      const float ty = (c & 8) ? mu * fzmin : ((c & 16) ? -mu * fzmin : 0.f);
-      const float* Bkk = Bg + kk * 144 + r * 12 + 3 * l;
-      acc = fmaf(Bkk[0], tx, acc);
-      acc = fmaf(Bkk[1], ty, acc);
-      acc = fmaf(Bkk[2], fzmin, acc);
+      if (t >= 0 && (s.code[t] & 1)) acc += s.G[t * 12 + r];
     }
     s.Dt[o] = acc;
   }
   for (int p = lane; p < NC; p += 64)
-    if (p >= nr) { s.v[p] = 0.f; s.g[p] = 0.f; s.dl[p] = 0.f; }
+    if (p >= nr) s.v[p] = 0.f;
   WSYNC();
   return nr;
 }
 
-// Polish check after refinement (E, L at the final v in LDS): KKT conditions per triple.
-// On success the triple's force is returned in (fx, fy, fz); the repaired face code of a
-// failing triple is left in s.tcnt.  Returns (all ok, any face changed) via `changed`.
+// Polish check after refinement (E, L at the final v in LDS): KKT conditions per triple
+// (lane t = triple t, its params from s.fpk).  On success the triple's force is written over
+// its ADMM primal s.x[3t .. 3t+2]; the repaired face code of a failing triple is left in
+// s.tcnt and `changed` says whether any face changed.
 template <int NC>
 __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
-                                             const float* __restrict__ Bg, const TripleFaces& tf,
-                                             float step, float& fx, float& fy, float& fz,
+                                             const float* __restrict__ Bg, int ntri, float step,
                                              bool& changed) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
-  fx = 0.f; fy = 0.f; fz = 0.f;
+  float fx = 0.f, fy = 0.f, fz = 0.f;
   float gx = 0.f, gy = 0.f, gz = 0.f;
-  const int k = tf.k, leg = tf.leg, sx = tf.sx, sy = tf.sy;
   WSYNC();
-  if (tf.owns) {
-    fz = tf.zl ? fzmin : s.v[tf.pz];
-    fx = (sx == 0) ? s.v[tf.px] : sx * mu * fz;
-    fy = (sy == 0) ? s.v[tf.py] : sy * mu * fz;
-    const float* Bk = Bg + k * 144;
+  const bool owns = lane < ntri;
+  const int code = owns ? s.code[lane] : 0;
+  const int kl = owns ? s.tri[lane] : 0;
+  const int k = kl >> 2, leg = kl & 3;
+  const int sx = (code & 2) ? 1 : ((code & 4) ? -1 : 0);
+  const int sy = (code & 8) ? 1 : ((code & 16) ? -1 : 0);
+  const bool zl = (code & 1) != 0;
+  if (owns) {
+    const int pk = s.fpk[lane];
+    const int px = pk & 255, py = (pk >> 8) & 255, pz = (pk >> 16) & 255;
+    fz = zl ? fzmin : s.v[pz];
+    fx = (sx == 0) ? s.v[px] : sx * mu * fz;
+    fy = (sy == 0) ? s.v[py] : sy * mu * fz;
+    const float* Bk = Bg + k * 144 + 3 * leg;
     float ax = 0.f, ay = 0.f, az = 0.f;
+#pragma unroll
     for (int r = 0; r < 12; ++r) {
       const float lr = s.L[12 * k + r];
-      ax = fmaf(Bk[r * 12 + 3 * leg], lr, ax);
-      ay = fmaf(Bk[r * 12 + 3 * leg + 1], lr, ay);
-      az = fmaf(Bk[r * 12 + 3 * leg + 2], lr, az);
+      ax = fmaf(Bk[r * 12], lr, ax);
+      ay = fmaf(Bk[r * 12 + 1], lr, ay);
+      az = fmaf(Bk[r * 12 + 2], lr, az);
     }
     gx = ax + s.R2[3 * leg] * fx;
     gy = ay + s.R2[3 * leg + 1] * fy;
@@ -716,24 +794,30 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   const float tol_d = P.polish_tol * gs, tol_p = P.polish_tol * us;
   bool ok = true;
   int nc = 0;
-  if (tf.owns) {
+  if (owns) {
     // KKT per triple; on a violation also derive the repaired face set (primal-dual
     // active-set step): drop faces with a negative multiplier, add violated faces
     const float lx = sx ? -sx * gx : 0.f;
     const float ly = sy ? -sy * gy : 0.f;
     const float l0 = gz - mu * (lx + ly);
-    nc = s.code[lane];
+    nc = code;
     if (sx && lx < -tol_d) { ok = false; nc &= ~6; }
     if (sy && ly < -tol_d) { ok = false; nc &= ~24; }
-    if (tf.zl && l0 < -tol_d) { ok = false; nc &= ~1; }
+    if (zl && l0 < -tol_d) { ok = false; nc &= ~1; }
     if (!sx && fabsf(fx) > mu * fz + tol_p) { ok = false; nc |= (fx > 0.f) ? 2 : 4; }
     if (!sy && fabsf(fy) > mu * fz + tol_p) { ok = false; nc |= (fy > 0.f) ? 8 : 16; }
-    if (!tf.zl && fz < fzmin - tol_p) { ok = false; nc |= 1; }
+    if (!zl && fz < fzmin - tol_p) { ok = false; nc |= 1; }
     if (!(isfinite(fx) && isfinite(fy) && isfinite(fz))) ok = false;
     s.tcnt[lane] = nc;  // repaired code (copied into s.code by the caller if used)
   }
-  changed = __any(tf.owns && nc != s.code[lane]) != 0;
-  return (__all(ok) != 0) && (step <= P.polish_tol * us);
+  changed = __any(owns && nc != code) != 0;
+  const bool all_ok = (__all(ok) != 0) && (step <= P.polish_tol * us);
+  if (all_ok && owns) {
+    s.x[3 * lane] = fx;
+    s.x[3 * lane + 1] = fy;
+    s.x[3 * lane + 2] = fz;
+  }
+  return all_ok;
 }
 
 // park / restore the register-resident inverse in the wave's global slab (uniform base,
@@ -777,7 +861,28 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   CMPC_CNT(10, 1);
 
   WSYNC();
-  for (int e = lane; e < 144; e += 64) s.A[e] = Ab[e];
+  {  // one round of global loads: A, r_0..r_N (= x0, xref), gd; staged in LDS (G is free here)
+    float av[3], rv[4];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = lane + 64 * i;
+      av[i] = (e < 144) ? Ab[e] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = lane + 64 * i;
+      rv[i] = (e < 12) ? x0b[e] : (e < 12 * (N + 1)) ? xrb[e - 12] : 0.f;
+    }
+    const float gv = (lane < 12) ? gdb[lane] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int e = lane + 64 * i;
+      if (e < 144) s.A[e] = av[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s.G[lane + 64 * i] = rv[i];
+    if (lane < 12) s.G[256 + lane] = gv;
+  }
   // stance triples in (k, leg) order; lane = 4k + leg
   const bool stc = (lane < 4 * N) ? (ctb[(lane & 3) * N + (lane >> 2)] != 0) : false;
   const int pos = wave_excl_scan4(stc ? 1 : 0);
@@ -787,27 +892,25 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   WSYNC();
   for (int o = lane; o < NP; o += 64) {  // d_k = A r_k + gd - r_{k+1}, r_0 = x0
     const int k = o / 12, r = o % 12;
-    const float* rk = (k == 0) ? x0b : (xrb + (k - 1) * 12);
-    float acc = gdb[r] - xrb[k * 12 + r];
+    const float* rk = &s.G[12 * k];
+    float acc = s.G[256 + r] - rk[12 + r];
 #pragma unroll
     for (int j = 0; j < 12; ++j) acc = fmaf(s.A[r * 12 + j], rk[j], acc);
     s.D[o] = acc;
   }
   build_admm_basis<NC>(s, P, Bg, ntri);
   const int n = 3 * ntri;
-  for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; }
+  for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; s.y[p] = 0.f; }
+  s.pcode[lane] = -1;
 
-  // ADMM state of this lane's triple (params 3*lane + a), in registers
-  float xs[3] = {0.f, 0.f, 0.f}, zs[3] = {0.f, 0.f, 0.f}, ys[3] = {0.f, 0.f, 0.f};
-  const bool mine = lane < ntri;
+  CMPC_ACC(6, t_inst);
+  // ADMM state (x, z, y of triple t at 3t .. 3t+2) lives in LDS, not in registers
 
   int status = -2, iters = 0;
   bool polished = false;
-  float pfx = 0.f, pfy = 0.f, pfz = 0.f;  // polished force of this lane's triple
-  TripleFaces tf;
   float rho = P.rho0;
   float rp = 0.f, rd = 0.f, np_ = 0.f, nd = 0.f;
-  int prev_code = -1, stable = 0;
+  int stable = 0;
   bool refactor = n > 0;  // (re)build + invert the matrix for the current basis
   bool in_polish = false;
   int nact = n;           // params of the current basis
@@ -843,7 +946,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       }
       gradient<NC>(s, P, nact, s.v, s.g);  // E, L at the final point
       bool changed = false;
-      const bool ok = polish_check<NC>(s, P, Bg, tf, step, pfx, pfy, pfz, changed);
+      const bool ok = polish_check<NC>(s, P, Bg, ntri, step, changed);
 #ifdef CMPC_TRACE
       if (b == CMPC_TRACE && lane == 0)
         printf("it %d polish nact %d ok %d changed %d step %g repairs_left %d\n", it, nact, (int)ok,
@@ -858,7 +961,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       if (repairs_left > 0 && changed) {  // re-polish on the repaired face set
         --repairs_left;
         if (lane < ntri) s.code[lane] = s.tcnt[lane];
-        nact = polish_setup<NC>(s, P, Bg, ntri, tf);
+        nact = polish_setup<NC>(s, P, Bg, ntri);
         shift = P.sigma;
         refactor = true;
         continue;
@@ -870,10 +973,6 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         refactor = true;
       }
       build_admm_basis<NC>(s, P, Bg, ntri);
-      if (mine) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) { s.x[3 * lane + a] = xs[a]; s.z[3 * lane + a] = zs[a]; }
-      }
       in_polish = false;
       nact = n;
       shift = P.sigma + rho;
@@ -883,47 +982,56 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     iters = it;
     // ---- one ADMM iteration ----
     gradient<NC>(s, P, n, s.x, s.g);
-    if (mine) {
+    {
+      const int l = opaque_lane();
+      if (l < ntri) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int p = 3 * lane + a;
-        s.r[p] = rho * (zs[a] - xs[a]) - s.g[p] - ys[a];
+        for (int a = 0; a < 3; ++a) {
+          const int p = 3 * l + a;
+          s.r[p] = rho * (s.z[p] - s.x[p]) - s.g[p] - s.y[p];
+        }
       }
     }
     symv<NC>(s, M, n, s.r, s.dl);
+    CMPC_T0(t_rest);
     const bool last = (it == P.max_iter);
     const bool adapt = P.adaptive_interval > 0 && (it % P.adaptive_interval) == 0;
     const float inv_rho = 1.f / rho;
-    int code = 0;
     float lrp = 0.f, lrd = 0.f, lnp = 0.f, lnd = 0.f;
-    if (mine) {
-      float w[3], xr[3];
+    bool changed = false;
+    {
+      const int l = opaque_lane();
+      if (l < ntri) {
+        float w[3], xr[3], xs[3];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int p = 3 * lane + a;
-        const float xt = xs[a] + s.dl[p];
-        xr[a] = alpha * xt + (1.f - alpha) * zs[a];
-        xs[a] = alpha * xt + (1.f - alpha) * xs[a];
-        w[a] = xr[a] + ys[a] * inv_rho;
-      }
-      float pv[3];
-      code = project(w[0], w[1], w[2], P.mu, P.fz_min, pv[0], pv[1], pv[2]);
+        for (int a = 0; a < 3; ++a) {
+          const int p = 3 * l + a;
+          const float x = s.x[p], z = s.z[p];
+          const float xt = x + s.dl[p];
+          xr[a] = alpha * xt + (1.f - alpha) * z;
+          xs[a] = alpha * xt + (1.f - alpha) * x;
+          w[a] = xr[a] + s.y[p] * inv_rho;
+        }
+        float pv[3];
+        const int code = project(w[0], w[1], w[2], P.mu, P.fz_min, pv[0], pv[1], pv[2]);
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int p = 3 * lane + a;
-        const float zn = pv[a];
-        const float yn = ys[a] + rho * (xr[a] - zn);
-        zs[a] = zn;
-        ys[a] = yn;
-        s.x[p] = xs[a];
-        s.z[p] = zn;
-        const float gp = s.g[p];
-        lrp = fmaxf(lrp, fabsf(xs[a] - zn));
-        lrd = fmaxf(lrd, fabsf(gp + yn));
-        lnp = fmaxf(lnp, fmaxf(fabsf(xs[a]), fabsf(zn)));
-        lnd = fmaxf(lnd, fmaxf(fabsf(gp), fabsf(yn)));
+        for (int a = 0; a < 3; ++a) {
+          const int p = 3 * l + a;
+          const float zn = pv[a];
+          const float yn = s.y[p] + rho * (xr[a] - zn);
+          s.x[p] = xs[a];
+          s.z[p] = zn;
+          s.y[p] = yn;
+          const float gp = s.g[p];
+          lrp = fmaxf(lrp, fabsf(xs[a] - zn));
+          lrd = fmaxf(lrd, fabsf(gp + yn));
+          lnp = fmaxf(lnp, fmaxf(fabsf(xs[a]), fabsf(zn)));
+          lnd = fmaxf(lnd, fmaxf(fabsf(gp), fabsf(yn)));
+        }
+        changed = code != s.pcode[l];
+        s.pcode[l] = code;
+        s.code[l] = code;
       }
-      s.code[lane] = code;
     }
 #ifdef CMPC_TRACE
     if (b == CMPC_TRACE) {
@@ -931,8 +1039,6 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       if (lane == 0) printf("it %d rho %g rp %g rd %g stable %d\n", it, rho, trp, trd, stable);
     }
 #endif
-    const bool changed = mine && (code != prev_code);
-    prev_code = code;
     stable = (__any(changed) != 0) ? 0 : stable + 1;
     bool do_pol = false;
     if (stable >= P.polish_stable && !last) {
@@ -951,11 +1057,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         refactor = true;
       }
     }
+    CMPC_ACC(7, t_rest);
     if (do_pol) {
       CMPC_CNT(9, 1);
+      CMPC_T0(t_ps);
       parked = !refactor;  // a pending refactor (rho changed) makes the current inverse stale
       if (parked) park_store<NC>(park, M);  // restored if the polish fails
-      nact = polish_setup<NC>(s, P, Bg, ntri, tf);
+      nact = polish_setup<NC>(s, P, Bg, ntri);
+      CMPC_ACC(14, t_ps);
       shift = P.sigma;
       refactor = true;
       in_polish = true;
@@ -966,36 +1075,23 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     if (n > 0) {
       const bool conv = rp <= P.eps_abs + P.eps_rel * np_ && rd <= P.eps_abs + P.eps_rel * nd;
       status = conv ? 2 : -2;
-      if (mine) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) s.z[3 * lane + a] = zs[a];
-      }
     }
     gradient<NC>(s, P, n, s.z, s.g);  // E at u = z (the pure rollout when every leg swings)
   }
+  CMPC_T0(t_out);
   // ---- outputs: x_{k+1} = e_{k+1} + xref_k, u from the triples (zero on swing legs) ----
   WSYNC();
   float* wb = out.w + b * (int64_t)(24 * N);
+  const float* uf = polished ? s.x : s.z;  // polished forces overwrote x; else u = z
   int bad = 0;
   for (int o = lane; o < NP; o += 64) {
     const float xv = s.E[o] + xrb[o];
-    bad |= !isfinite(xv);
-    wb[o] = xv;
     const int k = o / 12, l = (o % 12) / 3, a = o % 3;
     const int t = s.tri_of[4 * k + l];
-    if (!polished) {  // u = z (ADMM basis)
-      const float uv = (t >= 0) ? s.z[3 * t + a] : 0.f;
-      bad |= !isfinite(uv);
-      wb[NP + o] = uv;
-    } else if (t < 0) {  // swing leg; stance forces are written by the owning lane below
-      wb[NP + o] = 0.f;
-    }
-  }
-  if (polished && mine) {
-    const int kl = s.tri[lane];
-    float* ub = wb + NP + 12 * (kl >> 2) + 3 * (kl & 3);
-    ub[0] = pfx; ub[1] = pfy; ub[2] = pfz;
-    bad |= !(isfinite(pfx) && isfinite(pfy) && isfinite(pfz));
+    const float uv = (t >= 0) ? uf[3 * t + a] : 0.f;
+    bad |= !(isfinite(xv) && isfinite(uv));
+    wb[o] = xv;
+    wb[NP + o] = uv;
   }
   if (__any(bad)) status = -10;
   if (lane == 0) {
@@ -1003,6 +1099,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     out.iters[b] = iters;
   }
   CMPC_CNT(11, iters);
+  CMPC_ACC(15, t_out);
   CMPC_ACC(5, t_inst);
 }
 

@@ -14,5 +14,7 @@ run() {
 }
 run "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" && \
 run "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM SQ_WAIT_INST_LDS" && \
-run "FETCH_SIZE" && run "WRITE_SIZE" && run "GRBM_GUI_ACTIVE GRBM_COUNT"
+run "SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH SQ_INST_CYCLES_VMEM" && \
+run "GRBM_GUI_ACTIVE GRBM_COUNT"
+ls gpurun_out/pmc/*/ > /dev/null
 ls gpurun_out/pmc/*/

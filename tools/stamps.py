@@ -17,14 +17,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--lib", default=str(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_stamps.so"))
+    ap.add_argument("--only-bin", type=int, default=-1, help="keep only instances of this bin (0-3)")
     a = ap.parse_args()
     import torch
     from cmpc import _lib, synth
-    lib = _lib.load(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_stamps.so")
+    lib = _lib.load(Path(a.lib))
     _lib._lib = lib
     lib.cmpc_debug_stamps.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
     from cmpc import Plan, SolverParams, to_device_batch
     b = synth.make_batch(a.batch, seed=1, mixed=(a.config == 2))
+    if a.only_bin >= 0:
+        nf = 3 * (b["contact"] != 0).reshape(a.batch, -1).sum(1)
+        keep = np.searchsorted(np.array([96, 128, 160, 192]), nf) == a.only_bin
+        b = {k: (v[keep] if isinstance(v, np.ndarray) and v.shape[:1] == keep.shape else v) for k, v in b.items()}
+        a.batch = int(keep.sum())
+        print("instances kept:", a.batch)
     d = to_device_batch(b)
     plan = Plan(SolverParams(max_batch=a.batch))
     buf = (ctypes.c_ulonglong * 16)()
@@ -36,13 +44,16 @@ def main():
     lib.cmpc_debug_stamps(buf)
     v = np.array(list(buf), dtype=np.float64)
     n = v[10]
-    names = ["condense", "invert", "gradient", "symv", "polish(all)", "instance total",
-             " condense_stage", " gradient mfma"]
+    names = ["condense", "invert", "gradient", "symv", "polish(all, incl. grad/symv)",
+             "instance total", "setup", "admm rest", None, None, None, None, None, None,
+             "polish setup", "output"]
     print(f"instances {int(n)}  mean iters {v[11]/n:.2f}  condense_invert/inst {v[8]/n:.2f}  "
           f"polish attempts/inst {v[9]/n:.2f}")
     for i, nm in enumerate(names):
-        print(f"  {nm:16s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
-    print(f"  per call: condense {v[0]/v[8]:.0f}  stage {v[6]/v[8]:.0f}  invert {v[1]/v[8]:.0f}  gradient {v[2]/max(v[12],1):.0f} (mfma {v[7]/max(v[12],1):.0f}, x{v[12]/n:.1f})  symv {v[3]/max(v[13],1):.0f} (x{v[13]/n:.1f}) cycles")
+        if nm is None:
+            continue
+        print(f"  {nm:28s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
+    print(f"  per call: condense {v[0]/v[8]:.0f}  invert {v[1]/v[8]:.0f}  gradient {v[2]/max(v[12],1):.0f} (x{v[12]/n:.1f})  symv {v[3]/max(v[13],1):.0f} (x{v[13]/n:.1f}) cycles")
     print("  status:", dict(zip(*np.unique(st.cpu().numpy(), return_counts=True))))
 
 

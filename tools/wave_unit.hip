@@ -8,9 +8,9 @@ using namespace cmpc;
 
 // S: NC x NC row-major (only [0,n) used); out: NC x NC row-major inverse (lower tiles mirrored);
 // y = inv * x for x given (NC)
-__global__ void __launch_bounds__(64) k_invert(const float* S, int n, float* out, const float* x,
-                                               float* y) {
-  constexpr int NC = 128;
+template <int NC>
+__global__ void __launch_bounds__(64, Cfg<NC>::WPE) k_invert(const float* S, int n, float* out,
+                                                            const float* x, float* y) {
   using C = Cfg<NC>;
   __shared__ Smem<NC> s;
   const int lane = threadIdx.x, g = lane >> 4, c = lane & 15;
@@ -23,7 +23,7 @@ __global__ void __launch_bounds__(64) k_invert(const float* S, int n, float* out
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * I + 4 * g + q, col = 16 * J + c;
-        v[q] = (row < n && col < n) ? S[row * NC + col] : (row == col ? 1.f : 0.f);
+        v[q] = (row < n && col < n) ? S[row * 192 + col] : (row == col ? 1.f : 0.f);
       }
       M[tile_index(I, J)] = v;
     }
@@ -39,23 +39,26 @@ __global__ void __launch_bounds__(64) k_invert(const float* S, int n, float* out
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * I + 4 * g + q, col = 16 * J + c;
-        out[row * NC + col] = v[q];
-        out[col * NC + row] = v[q];
+        out[row * 192 + col] = v[q];
+        out[col * 192 + row] = v[q];
       }
     }
 }
 
 extern "C" int wave_invert(const float* S, int n, float* out, const float* x, float* y) {
   float *dS, *dO, *dx, *dy;
-  const size_t bytes = 128 * 128 * 4;
+  const size_t bytes = 192 * 192 * 4;
   (void)hipMalloc(&dS, bytes); (void)hipMalloc(&dO, bytes);
-  (void)hipMalloc(&dx, 512); (void)hipMalloc(&dy, 512);
+  (void)hipMalloc(&dx, 768); (void)hipMalloc(&dy, 768);
   (void)hipMemcpy(dS, S, bytes, hipMemcpyHostToDevice);
-  (void)hipMemcpy(dx, x, 512, hipMemcpyHostToDevice);
-  hipLaunchKernelGGL(k_invert, dim3(1), dim3(64), 0, 0, dS, n, dO, dx, dy);
+  (void)hipMemcpy(dx, x, 768, hipMemcpyHostToDevice);
+  (void)hipMemset(dO, 0, bytes);
+  if (n <= 128) hipLaunchKernelGGL(k_invert<128>, dim3(1), dim3(64), 0, 0, dS, n, dO, dx, dy);
+  else if (n <= 160) hipLaunchKernelGGL(k_invert<160>, dim3(1), dim3(64), 0, 0, dS, n, dO, dx, dy);
+  else hipLaunchKernelGGL(k_invert<192>, dim3(1), dim3(64), 0, 0, dS, n, dO, dx, dy);
   hipError_t e = hipDeviceSynchronize();
   (void)hipMemcpy(out, dO, bytes, hipMemcpyDeviceToHost);
-  (void)hipMemcpy(y, dy, 512, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(y, dy, 768, hipMemcpyDeviceToHost);
   (void)hipFree(dS); (void)hipFree(dO); (void)hipFree(dx); (void)hipFree(dy);
   return (int)e;
 }

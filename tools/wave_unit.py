@@ -5,26 +5,26 @@ from pathlib import Path
 
 import numpy as np
 
-lib = ctypes.CDLL(str(Path(__file__).resolve().parent / "libwave_unit.so"))
+lib = ctypes.CDLL(str(Path(__file__).resolve().parent / (sys.argv[1] if len(sys.argv) > 1 else "libwave_unit.so")))
 P = ctypes.POINTER(ctypes.c_float)
 lib.wave_invert.argtypes = [P, ctypes.c_int, P, P, P]
 rng = np.random.default_rng(0)
-for n in (1, 4, 5, 16, 17, 63, 100, 115, 128):
+for n in (1, 4, 5, 16, 17, 63, 100, 115, 128, 129, 141, 150, 160, 161, 180, 192):
     A = rng.standard_normal((n, n))
     S = A @ A.T + n * np.eye(n) * 0.5
-    S32 = np.zeros((128, 128), np.float32)
+    S32 = np.zeros((192, 192), np.float32)
     S32[:n, :n] = S
-    x = np.zeros(128, np.float32)
+    x = np.zeros(192, np.float32)
     x[:n] = rng.standard_normal(n)
-    out = np.zeros((128, 128), np.float32)
-    y = np.zeros(128, np.float32)
+    out = np.zeros((192, 192), np.float32)
+    y = np.zeros(192, np.float32)
     rc = lib.wave_invert(S32.ctypes.data_as(P), n, out.ctypes.data_as(P), x.ctypes.data_as(P),
                          y.ctypes.data_as(P))
     inv = np.linalg.inv(S)
     e_inv = np.max(np.abs(out[:n, :n] - inv)) / np.max(np.abs(inv))
     e_y = np.max(np.abs(y[:n] - inv @ x[:n])) / np.max(np.abs(inv @ x[:n]))
     print(f"n={n:4d} rc={rc} inverse rel err {e_inv:.2e}  symv rel err {e_y:.2e}  "
-          f"pad max {np.max(np.abs(y[n:])) if n < 128 else 0:.1e}")
+          f"pad max {np.max(np.abs(y[n:])) if n < 192 else 0:.1e}")
     sys.stdout.flush()
 
 # condensation vs tests/algo_spec.condense on fixture instances
@@ -85,8 +85,8 @@ for name in ("qp_cfg1.npz", "qp_cfg2.npz"):
         Bt = [B[k][:, [3 * l + a for l in range(4) if st[k, l] for a in range(3)]] for k in range(16)]
         Rt = np.concatenate([pr.R[3 * l:3 * l + 3] for k in range(16) for l in range(4) if st[k, l]])
         H = algo_spec.condense(A, Bt, pr.Q, Rt, 1e-6).astype(np.float64)
-        S32 = np.zeros((128, 128), np.float32); S32[:nf, :nf] = H
-        out = np.zeros((128, 128), np.float32); x = np.zeros(128, np.float32); y = np.zeros(128, np.float32)
+        S32 = np.zeros((192, 192), np.float32); S32[:nf, :nf] = H
+        out = np.zeros((192, 192), np.float32); x = np.zeros(192, np.float32); y = np.zeros(192, np.float32)
         lib.wave_invert(S32.ctypes.data_as(P), nf, out.ctypes.data_as(P), x.ctypes.data_as(P), y.ctypes.data_as(P))
         Mi = out[:nf, :nf].astype(np.float64)
         rad = np.max(np.abs(np.linalg.eigvals(np.eye(nf) - Mi @ H)))
