@@ -34,6 +34,7 @@ def build_library(force: bool = False, verbose: bool = False) -> Path:
         return LIB
     LIB.parent.mkdir(parents=True, exist_ok=True)
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-fno-slp-vectorize",  # keep f32 adds scalar so DPP operands fuse (no v_pk_*)
            f"-I{REPO / 'include'}", f"-I{CSRC}", *map(str, SOURCES), "-o", str(LIB) + ".tmp"]
     if verbose:
         print(" ".join(cmd))

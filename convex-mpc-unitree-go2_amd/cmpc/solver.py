@@ -38,7 +38,7 @@ class SolverParams:
     polish_stable: int = 3
     polish_refine: int = 4
     polish_tol: float = 1e-5
-    polish_repairs: int = 3
+    polish_repairs: int = 6
     max_batch: int = 65536
 
     def to_c(self) -> _lib.CParams:

@@ -20,9 +20,15 @@ struct cmpc_plan {
   int device;
   int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
-  float* d_work;    // per-workgroup park slabs (largest bin's need)
+  float* d_work;    // per-wave park slabs; bin q's region starts at work_off[q] (bins run concurrently)
+  size_t work_off[cmpc::kNumBins];
   int grid[cmpc::kNumBins];
   int threads[cmpc::kNumBins];
+  // per-bin streams: the bins' persistent kernels run concurrently so one bin's tail (its last
+  // long-running instances) overlaps the other bins' work; forked from / joined to the caller
+  hipStream_t bin_stream[cmpc::kNumBins] = {};
+  hipEvent_t fork = nullptr;
+  hipEvent_t join[cmpc::kNumBins] = {};
   // timing hooks
   bool timing = false;
   struct Rec { hipEvent_t a, b; int bin; };
@@ -97,7 +103,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_stable = 3;
   p->polish_refine = 4;
   p->polish_tol = 1e-5f;
-  p->polish_repairs = 3;
+  p->polish_repairs = 6;
   p->max_batch = 65536;
 }
 
@@ -165,8 +171,8 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     }
 #endif
     pl->grid[q] = nb * cus;
-    const size_t need = (size_t)pl->grid[q] * bin_slab(q);
-    if (need > work_floats) work_floats = need;
+    pl->work_off[q] = work_floats;
+    work_floats += (size_t)pl->grid[q] * bin_slab(q);
   }
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
@@ -182,6 +188,17 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     (void)hipFree(pl->d_work);
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
+  }
+  for (int q = 0; q < cmpc::kNumBins; ++q) {
+    if ((e = hipStreamCreateWithFlags(&pl->bin_stream[q], hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&pl->join[q], hipEventDisableTiming)) != hipSuccess) {
+      cmpc_plan_destroy(pl);
+      return hip_fail(e, "bin stream/event creation");
+    }
+  }
+  if ((e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess) {
+    cmpc_plan_destroy(pl);
+    return hip_fail(e, "hipEventCreateWithFlags");
   }
   *out = pl;
   g_err.clear();
@@ -208,11 +225,15 @@ int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const
   if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
   cmpc::Inputs in{Ad, Bd, gd, x0, xref, contact};
   cmpc::Outputs out{w_out, status, iters};
+  if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  int launched[cmpc::kNumBins] = {0};
   for (int q = 0; q < cmpc::kNumBins; ++q) {
     const int cap = cmpc::kBinCap[q];
     if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) break;  // bins beyond 12N are empty
     (void)cap;
     const long long g = pl->grid[q] < B ? pl->grid[q] : B;
+    hipStream_t bs = pl->bin_stream[q];
+    if ((e = hipStreamWaitEvent(bs, pl->fork, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
     cmpc_plan::Rec rec{nullptr, nullptr, q};
     const bool rec_this = pl->timing && pl->recs.size() < 4096 * cmpc::kNumBins;
     if (rec_this) {
@@ -224,17 +245,24 @@ int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const
         if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
         if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
       }
-      if ((e = hipEventRecord(rec.a, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+      if ((e = hipEventRecord(rec.a, bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     }
-    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(pl->threads[q]), 0, st, pl->kp, in,
+    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(pl->threads[q]), 0, bs, pl->kp, in,
                        out, pl->d_lists + (size_t)q * pl->p.max_batch, pl->d_counters + q,
-                       pl->d_counters + cmpc::kNumBins + q, pl->d_work);
+                       pl->d_counters + cmpc::kNumBins + q, pl->d_work + pl->work_off[q]);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "solve_bin_kernel launch");
     if (rec_this) {
-      if ((e = hipEventRecord(rec.b, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+      if ((e = hipEventRecord(rec.b, bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
       pl->recs.push_back(rec);
     }
+    if ((e = hipEventRecord(pl->join[q], bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    launched[q] = 1;
+  }
+  for (int q = 0; q < cmpc::kNumBins; ++q) {
+    if (!launched[q]) continue;
+    if ((e = hipStreamWaitEvent(st, pl->join[q], 0)) != hipSuccess)
+      return hip_fail(e, "hipStreamWaitEvent");
   }
   return CMPC_OK;
 }
@@ -267,6 +295,11 @@ void cmpc_plan_destroy(cmpc_plan* pl) {
   if (!pl) return;
   for (auto& r : pl->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto& r : pl->pool) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  for (int q = 0; q < cmpc::kNumBins; ++q) {
+    if (pl->bin_stream[q]) (void)hipStreamDestroy(pl->bin_stream[q]);
+    if (pl->join[q]) (void)hipEventDestroy(pl->join[q]);
+  }
+  if (pl->fork) (void)hipEventDestroy(pl->fork);
   (void)hipFree(pl->d_counters);
   (void)hipFree(pl->d_lists);
   (void)hipFree(pl->d_work);
