@@ -162,17 +162,20 @@ def main():
         tj = json.loads(Path(args.traffic_json).read_text())
         traffic = tj.get("hbm_bytes_per_launch")
 
-    # latency of one small batch (configs[1]: B=256) on the same plan
+    # latency of one small batch (configs[1]: B=256) on the same plan (0: skip, e.g. under a
+    # profiler so that every traced launch is a full-batch step)
     lb = min(args.latency_batch, B)
+    lat_ms = None
     sl = {k: v[:lb] for k, v in d.items()}
-    for _ in range(3):
-        plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
-    torch.cuda.synchronize(dev)
-    tl0 = time.perf_counter()
-    for _ in range(10):
-        plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
-    torch.cuda.synchronize(dev)
-    lat_ms = (time.perf_counter() - tl0) / 10 * 1e3
+    if lb > 0:
+        for _ in range(3):
+            plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
+        torch.cuda.synchronize(dev)
+        tl0 = time.perf_counter()
+        for _ in range(10):
+            plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
+        torch.cuda.synchronize(dev)
+        lat_ms = (time.perf_counter() - tl0) / 10 * 1e3
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

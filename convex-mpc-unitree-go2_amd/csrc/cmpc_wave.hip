@@ -1061,8 +1061,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     if (do_pol) {
       CMPC_CNT(9, 1);
       CMPC_T0(t_ps);
+#ifndef CMPC_NO_PARK
       parked = !refactor;  // a pending refactor (rho changed) makes the current inverse stale
       if (parked) park_store<NC>(park, M);  // restored if the polish fails
+#else
+      parked = false;      // a failed polish refactors the ADMM matrix instead
+#endif
       nact = polish_setup<NC>(s, P, Bg, ntri);
       CMPC_ACC(14, t_ps);
       shift = P.sigma;
