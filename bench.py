@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--traffic-json", type=str, default=str(REPO / "profiles" / "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
     ap.add_argument("--latency-batch", type=int, default=256)
+    ap.add_argument("--dynamics-steps", type=int, default=5,
+                    help="timed steps of the on-device dynamics build (+ fused build+solve); 0 = skip")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     return ap.parse_args()
@@ -177,6 +179,42 @@ def main():
         torch.cuda.synchronize(dev)
         lat_ms = (time.perf_counter() - tl0) / 10 * 1e3
 
+    # the discrete dynamics built on the device (cmpc_build_dynamics) --
+    # its own HBM roofline, and the fused per-tick throughput build + solve
+    dyn = None
+    if args.dynamics_steps > 0:
+        N = 16
+        dm = {k: torch.as_tensor(batch[k], dtype=torch.float32).contiguous().to(dev)
+              for k in ("m", "I_world", "r_legs")}
+        dt = float(batch["dt"])
+        outs = (torch.empty_like(d["Ad"]), torch.empty_like(d["Bd"]), torch.empty_like(d["gd"]))
+        for _ in range(2):
+            plan.build_dynamics(dm["m"], dm["I_world"], dm["r_legs"], d["xref"], dt, out=outs,
+                                stream=stream)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.dynamics_steps):
+            plan.build_dynamics(dm["m"], dm["I_world"], dm["r_legs"], d["xref"], dt, out=outs,
+                                stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        dyn_ms = e0.elapsed_time(e1) / args.dynamics_steps
+        dyn_bytes = B * (4 + 36 + N * 48 + N * 48 + 576 + N * 576 + 48)
+        t0f = time.perf_counter()
+        for _ in range(args.dynamics_steps):
+            plan.build_dynamics(dm["m"], dm["I_world"], dm["r_legs"], d["xref"], dt, out=outs,
+                                stream=stream)
+            plan.solve(outs[0], outs[1], outs[2], d["x0"], d["xref"], d["contact"],
+                       out=(w, st, it), stream=stream)
+        torch.cuda.synchronize(dev)
+        fused = B * args.dynamics_steps / (time.perf_counter() - t0f)
+        gbs = dyn_bytes / (dyn_ms * 1e-3) / 1e9
+        dyn = {"kernel": "dynamics_kernel", "ms_per_step": dyn_ms, "robots_per_s": B / (dyn_ms * 1e-3),
+               "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": gbs / HBM_PEAK_GBS, "bytes_per_robot": dyn_bytes // B},
+               "fused_build_and_solve_per_s": fused}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, args.cpu_seconds)
@@ -213,6 +251,7 @@ def main():
             "solved_frac": solved_frac,
             "iters_mean": float(np.mean(iters)),
             "latency_ms_b256": lat_ms,
+            "dynamics": dyn,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},
             "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},

@@ -154,6 +154,41 @@ class Plan:
         _check(self.lib, rc, "cmpc_solve")
         return w, status, iters
 
+    def build_dynamics(self, mass, inertia, r_feet, xref, dt, out=None, stream=None):
+        """Discrete dynamics (Ad, Bd, gd) of B robots on the device -- the reference's
+        ComTraj._continuousDynamics + _discreteDynamics (com_trajectory.py:221-286) in closed
+        form.  mass (B,), inertia (B,3,3) I_com_world, r_feet (B,N,4,3) COM->foot lever arms
+        (legs FL FR RL RR), xref (B,N,12) as for solve(); all fp32 device tensors."""
+        N = self.params.N
+        B = mass.shape[0]
+        f32 = torch.float32
+        _dev_tensor(mass, "mass", f32, (B,))
+        _dev_tensor(inertia, "inertia", f32, (B, 3, 3))
+        _dev_tensor(r_feet, "r_feet", f32, (B, N, 4, 3))
+        _dev_tensor(xref, "xref", f32, (B, N, 12))
+        for t in (inertia, r_feet, xref):
+            if t.device != mass.device:
+                raise ValueError("all inputs must be on the same device")
+        if out is None:
+            Ad = torch.empty((B, 12, 12), dtype=f32, device=mass.device)
+            Bd = torch.empty((B, N, 12, 12), dtype=f32, device=mass.device)
+            gd = torch.empty((B, 12), dtype=f32, device=mass.device)
+        else:
+            Ad, Bd, gd = out
+            _dev_tensor(Ad, "Ad", f32, (B, 12, 12))
+            _dev_tensor(Bd, "Bd", f32, (B, N, 12, 12))
+            _dev_tensor(gd, "gd", f32, (B, 12))
+        if stream is None:
+            stream = torch.cuda.current_stream(mass.device)
+        sp = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        with torch.cuda.device(mass.device):
+            rc = self.lib.cmpc_build_dynamics(
+                self._h, ctypes.c_int64(B), ctypes.c_float(dt),
+                *[ctypes.c_void_p(t.data_ptr()) for t in (mass, inertia, r_feet, xref, Ad, Bd, gd)],
+                sp)
+        _check(self.lib, rc, "cmpc_build_dynamics")
+        return Ad, Bd, gd
+
 
 def to_device_batch(batch: dict, device="cuda") -> dict:
     """float64/uint8 numpy batch (cmpc.synth layout) -> contiguous device tensors."""

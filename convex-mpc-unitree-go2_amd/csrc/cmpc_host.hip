@@ -12,7 +12,8 @@
 #include "cmpc.h"
 #include "cmpc_device.h"
 
-#include "cmpc_wave.hip"  // kernels: same translation unit
+#include "cmpc_wave.hip"      // solve kernels: same translation unit
+#include "cmpc_dynamics.hip"  // QP-data (discrete dynamics) kernel
 
 struct cmpc_plan {
   cmpc_params p;
@@ -264,6 +265,24 @@ int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const
     if ((e = hipStreamWaitEvent(st, pl->join[q], 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
   }
+  return CMPC_OK;
+}
+
+int cmpc_build_dynamics(cmpc_plan* pl, int64_t B, float dt, const float* mass,
+                        const float* inertia, const float* r_feet, const float* xref, float* Ad,
+                        float* Bd, float* gd, void* stream) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_build_dynamics: null plan");
+  if (B < 0) return fail(CMPC_E_INVALID, "cmpc_build_dynamics: negative batch");
+  if (!(dt > 0.f) || !std::isfinite(dt)) return fail(CMPC_E_INVALID, "cmpc_build_dynamics: dt must be > 0");
+  if (B == 0) return CMPC_OK;
+  if (!mass || !inertia || !r_feet || !xref || !Ad || !Bd || !gd)
+    return fail(CMPC_E_INVALID, "cmpc_build_dynamics: null array argument");
+  const long long blocks = B < 8192 ? B : 8192;  // grid-stride: ~32 resident waves per CU
+  hipLaunchKernelGGL(cmpc::dynamics_kernel, dim3((unsigned)blocks), dim3(64), 0,
+                     (hipStream_t)stream, pl->kp.N, (double)dt, B, mass, inertia, r_feet, xref, Ad,
+                     Bd, gd);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "dynamics_kernel launch");
   return CMPC_OK;
 }
 

@@ -96,9 +96,27 @@ int cmpc_solve(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd, con
 
 void cmpc_plan_destroy(cmpc_plan* plan);
 
+/* QP data on the device: the reference's discrete dynamics
+ * (com_trajectory.py:221-286, _continuousDynamics + _discreteDynamics) for B robots, in closed
+ * form.  Ac is nilpotent (Ac^2 = 0), so the ZOH of com_trajectory.py:278 is exactly
+ * Ad = I + Ac dt, Bd_k = (I dt + Ac dt^2/2) Bc_k, and the 50-sample trapezoid of :281-284 is
+ * exact for its linear integrand: gd = (I dt + Ac dt^2/2) gc.  Computed in fp64, stored fp32.
+ *   mass    [B]            fp32   go2.data.Ig.mass (com_trajectory.py:39)
+ *   inertia [B][3][3]      fp32   I_com_world (com_trajectory.py:40); inverted on the device
+ *   r_feet  [B][N][4][3]   fp32   lever arms COM -> foot in the world frame, legs FL FR RL RR
+ *                                 (r_*_foot_world[:, k], com_trajectory.py:108-207, 242-245)
+ *   xref    [B][N][12]     fp32   as for cmpc_solve; yaw_avg = mean_k xref[b][k][5]
+ *                                 (np.average(rpy_traj_world[2, :]), com_trajectory.py:226)
+ *   Ad, Bd, gd                    outputs, in cmpc_solve's input layouts
+ * N is the plan's horizon; dt > 0 (com_trajectory.py:210, time_step).  Asynchronous on
+ * `stream`; the outputs can be passed straight to cmpc_solve on the same stream. */
+int cmpc_build_dynamics(cmpc_plan* plan, int64_t B, float dt, const float* mass,
+                        const float* inertia, const float* r_feet, const float* xref,
+                        float* Ad, float* Bd, float* gd, void* stream);
+
 /* Measurement hooks (not on the reference's interface; used by bench.py).  While enabled,
- * cmpc_solve records a hipEvent pair on `stream` around every solve-kernel launch (one per
- * free-variable bin).  cmpc_plan_timing_read waits for the recorded events, returns the
+ * cmpc_solve records a hipEvent pair around every solve-kernel launch (one per free-variable
+ * bin; the bins run concurrently on plan-internal streams joined back to `stream`).  cmpc_plan_timing_read waits for the recorded events, returns the
  * summed kernel milliseconds per bin (ms_per_bin[4]) and launch counts (calls_per_bin[4]) since
  * the last read, and resets them.  At most 4096 solve calls are recorded between reads. */
 int cmpc_plan_set_timing(cmpc_plan* plan, int enable);

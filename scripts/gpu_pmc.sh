@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:-"--batch 16384 --steps 2 --warmup 1 --cpu-seconds 0"}
+ARGS=${BENCH_ARGS:-"--batch 65536 --steps 2 --warmup 1 --cpu-seconds 0 --latency-batch 0"}
 timeout -k 10 120 rocprofv3 -L > gpurun_out/pmc/counters.txt 2>&1 || true
 i=0
 for grp in "${PMC_GROUPS[@]:-}"; do :; done
