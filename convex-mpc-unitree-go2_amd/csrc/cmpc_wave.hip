@@ -336,21 +336,25 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
   }
   const int ng = (n + 3) >> 2;
   const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
-  for (int st = 0; st < ng; ++st) {
-    const int k0 = 4 * st, K = k0 >> 4, c0 = k0 & 15, gp = c0 >> 2;
-    const int pc = c - c0;
-    const bool colw = pc >= 0 && pc < 4, roww = g == gp;
-    // publish the 4 pivot columns (current values) as panel rows [row][0..3]: column part from
-    // tiles (I >= K, K), row part (transposed) from tiles (K, J < K); every panel row is
-    // rewritten each step, padding rows included.  One uniform branch selects K's tiles.
+  // The pivot-block column K is a compile-time constant of the outer (unrolled) loop, so the
+  // panel publish, the P^ identity and the diagonal fix address their tiles directly (no
+  // runtime dispatch over register tiles); the four 4-pivot steps inside a tile column are a
+  // runtime loop.
 #pragma unroll
-    for (int KK = 0; KK < C::TT; ++KK) {
-      if (KK != K) continue;
+  for (int K = 0; K < C::TT; ++K) {
+    if (4 * K >= ng) continue;  // uniform; `continue` keeps the unrolled loop's tiles static
+    const int subs = (ng - 4 * K) < 4 ? (ng - 4 * K) : 4;
+    for (int sub = 0; sub < subs; ++sub) {
+      const int c0 = 4 * sub, k0 = 16 * K + c0;
+      const int pc = c - c0;
+      const bool colw = pc >= 0 && pc < 4, roww = g == sub;
+      // publish the 4 pivot columns (P^ = P - I on the pivot rows) as panel rows [row][0..3]:
+      // column part from tiles (I >= K, K), row part (transposed) from tiles (K, J < K)
       if (colw) {
 #pragma unroll
-        for (int I = KK; I < C::TT; ++I) {
-          f4 m = M[tile_index(I, KK)];
-          if (I == KK) {  // P^ = P - I on the 4 pivot rows
+        for (int I = K; I < C::TT; ++I) {
+          f4 m = M[tile_index(I, K)];
+          if (I == K) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) m[q] -= (4 * g + q == c) ? 1.f : 0.f;
           }
@@ -360,58 +364,67 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
       }
       if (roww) {
 #pragma unroll
-        for (int J = 0; J < KK; ++J)
-          *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(KK, J)];
+        for (int J = 0; J < K; ++J)
+          *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(K, J)];
       }
-    }
-    WSYNC();
-    // D = L diag(dl) L' (unit lower L), so P^ D^-1 P^' = Y diag(1/dl) Y' with Y = P^ L^-T: the
-    // columns of Y are the pivot columns as the scalar sweep would see them (each already
-    // eliminated by the earlier pivots of the step), which keeps the scalar sweep's accuracy.
-    float Dm[16];  // the panel holds P^ = P - I: add the identity back for D
+      WSYNC();
+      // D = L diag(dl) L' (unit lower L), so P^ D^-1 P^' = Y diag(1/dl) Y' with Y = P^ L^-T: the
+      // columns of Y are the pivot columns as the scalar sweep would see them (each already
+      // eliminated by the earlier pivots of the step), which keeps the scalar sweep's accuracy.
+      float Dm[16];  // the panel holds P^ = P - I: add the identity back for D
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f4 rrow = *reinterpret_cast<const f4*>(&s.pan[(k0 + i) * 4]);
+      for (int i = 0; i < 4; ++i) {
+        const f4 rrow = *reinterpret_cast<const f4*>(&s.pan[(k0 + i) * 4]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j] + ((i == j) ? 1.f : 0.f);
-    }
-    const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
-    const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
-    const float i1 = __builtin_amdgcn_rcpf(Dm[5] - l10 * Dm[4]);
-    const float u21 = Dm[9] - l20 * Dm[4], u31 = Dm[13] - l30 * Dm[4];
-    const float l21 = u21 * i1, l31 = u31 * i1;
-    const float i2 = __builtin_amdgcn_rcpf(Dm[10] - l20 * Dm[8] - l21 * u21);
-    const float u32 = Dm[14] - l30 * Dm[8] - l31 * u21;
-    const float l32 = u32 * i2;
-    const float i3 = __builtin_amdgcn_rcpf(Dm[15] - l30 * Dm[12] - l31 * u31 - l32 * u32);
-    const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
-    float a[C::TT], b[C::TT];
-#pragma unroll
-    for (int I = 0; I < C::TT; ++I) {
-      const f4 ph = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
-      const float y0 = ph[0];
-      const float y1 = ph[1] - l10 * y0;
-      const float y2 = ph[2] - l20 * y0 - l21 * y1;
-      const float y3 = ph[3] - l30 * y0 - l31 * y1 - l32 * y2;
-      const float yg = g3 ? y3 : g2 ? y2 : g1 ? y1 : y0;
-      a[I] = -yg;
-      b[I] = yg * ig;
-    }
-#pragma unroll
-    for (int I = 0; I < C::TT; ++I) {
-      if (I >= TA) continue;  // uniform
-#pragma unroll
-      for (int J = 0; J <= I; ++J) {
-        const int t = tile_index(I, J);
-        M[t] = mfma4(a[I], b[J], M[t]);
+        for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j] + ((i == j) ? 1.f : 0.f);
       }
-    }
+      const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
+      const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
+      const float i1 = __builtin_amdgcn_rcpf(Dm[5] - l10 * Dm[4]);
+      const float u21 = Dm[9] - l20 * Dm[4], u31 = Dm[13] - l30 * Dm[4];
+      const float l21 = u21 * i1, l31 = u31 * i1;
+      const float i2 = __builtin_amdgcn_rcpf(Dm[10] - l20 * Dm[8] - l21 * u21);
+      const float u32 = Dm[14] - l30 * Dm[8] - l31 * u21;
+      const float l32 = u32 * i2;
+      const float i3 = __builtin_amdgcn_rcpf(Dm[15] - l30 * Dm[12] - l31 * u31 - l32 * u32);
+      // y_g = (P^ L^-T)_g = sum_m L^-1[g][m] P^_m: this lane's row of L^-1 (unit lower) and
+      // 1/dl_g, selected once per step, so each panel row costs four FMAs and no branches
+      const float n10 = -l10, n21 = -l21, n32 = -l32;
+      const float n20 = l21 * l10 - l20, n31 = l32 * l21 - l31;
+      const float n30 = -l30 - l31 * n10 - l32 * n20;
+      const float w0 = g3 ? n30 : g2 ? n20 : g1 ? n10 : 1.f;
+      const float w1 = g3 ? n31 : g2 ? n21 : g1 ? 1.f : 0.f;
+      const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
+      const float w3 = g3 ? 1.f : 0.f;
+      const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
+      f4 ph[C::TT];
 #pragma unroll
-    for (int KK = 0; KK < C::TT; ++KK) {  // -2 on the 4 pivot diagonals
-      if (KK != K) continue;
-      f4& m = M[tile_index(KK, KK)];
+      for (int I = 0; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
+      float a[C::TT], b[C::TT];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
+      for (int I = 0; I < C::TT; ++I) {
+        const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
+        a[I] = -yg;
+        b[I] = yg * ig;
+      }
+#pragma unroll
+      for (int I = 0; I < C::TT; ++I) {
+        if (I >= TA) continue;  // uniform
+#pragma unroll
+        for (int J = 0; J <= I; ++J) {
+          const int t = tile_index(I, J);
+#ifndef CMPC_EXP_INV_NO_MFMA
+          M[t] = mfma4(a[I], b[J], M[t]);
+#else
+          M[t][0] += a[I] * b[J];
+#endif
+        }
+      }
+      {  // -2 on the 4 pivot diagonals
+        f4& m = M[tile_index(K, K)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
+      }
     }
   }
   // M holds -(scaled inverse): undo sign and scaling
