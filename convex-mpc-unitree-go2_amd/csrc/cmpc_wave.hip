@@ -217,11 +217,13 @@ __device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * 
 // condensation straight into the register tiles (MFMA)
 // ------------------------------------------------------------------------------------------
 // H = sum_t G_t' Q2 G_t + diag(Rt) + shift, where G_t (12 x n) column p is A^{t - k_p} b_p
-// for k_p <= t and 0 otherwise (the prediction matrix row block of step t).  Walking t
-// forward, G_t = A G_{t-1} (three MFMAs per 16-column chunk, K = 12) plus the new columns of
-// step t; each lower tile (I, J) accumulates (Q2 G_t)_I' (G_t)_J with three MFMAs whose
-// accumulator IS the tile (lane (g, c): rows 4g..4g+3, column c).  Tile row I starts to
-// receive terms at the step of its first parameter.
+// for k_p <= t and 0 otherwise (the prediction-matrix row block of step t).  G_t lives in
+// REGISTERS as one accumulator tile per 16-column chunk (lane (g, c): states 4g..4g+3 of
+// column 16 J + c), with the state index permuted k = 4g + q across the four MFMA steps so that
+// an accumulator is directly the next product's B operand: G_{t+1} = A G_t is a chain of four
+// MFMAs per chunk, and every lower tile (I, J) accumulates (Q2 G_t)_I' (G_t)_J with four MFMAs
+// whose accumulator IS the matrix tile.  Tile row I starts to receive terms at the step of its
+// first parameter; nothing of G ever goes through memory.
 template <int NC>
 __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
                                                f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
@@ -230,54 +232,51 @@ __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
   const int g = lane >> 4, c = lane & 15;
   const int N = P.N;
   n = uniform(n);
-  const int TA = (n + 15) >> 4;
 #pragma unroll
   for (int t = 0; t < C::NTL; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int e = lane; e < NC * 12; e += 64) s.G[e] = 0.f;
-  float aA[3], q2[3];  // A[c][4st + g] (A operand of A G), Q2[4st + g]
+  float aA[4], q2[4];  // A operand of A G: A[c][4g + q]; Q2[4g + q]
 #pragma unroll
-  for (int st = 0; st < 3; ++st) {
-    aA[st] = (c < 12) ? s.A[c * 12 + 4 * st + g] : 0.f;
-    q2[st] = s.Q2[4 * st + g];
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * g + q;
+    aA[q] = (c < 12 && r < 12) ? s.A[c * 12 + r] : 0.f;
+    q2[q] = (r < 12) ? s.Q2[r] : 0.f;
   }
   int kI[C::TT];  // first step of tile row I (N: no parameters)
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) kI[I] = (16 * I < n) ? s.par[16 * I] : N;
+  f4 Gd[C::TT];
+#pragma unroll
+  for (int J = 0; J < C::TT; ++J) Gd[J] = f4{0.f, 0.f, 0.f, 0.f};
   for (int t = 0; t < N; ++t) {
-    WSYNC();
     if (t > 0) {  // G_t = A G_{t-1} on the chunks that already hold columns
 #pragma unroll
-      for (int ch = 0; ch < C::TT; ++ch) {
-        if (kI[ch] >= t) continue;  // uniform
-        const float* col = &s.G[(16 * ch + c) * 12];
+      for (int J = 0; J < C::TT; ++J) {
+        if (kI[J] >= t) continue;  // uniform
         f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int st = 0; st < 3; ++st) d = mfma4(aA[st], col[4 * st + g], d);
-        if (g < 3) *reinterpret_cast<f4*>(&s.G[(16 * ch + c) * 12 + 4 * g]) = d;
+        for (int q = 0; q < 4; ++q) d = mfma4(aA[q], Gd[J][q], d);
+        Gd[J] = d;
       }
-      WSYNC();
     }
-    const int p0 = s.off[t], m = s.off[t + 1] - p0;  // new columns b_p of step t
-    for (int e = lane; e < 12 * m; e += 64) s.G[p0 * 12 + e] = s.Bt[p0 * 12 + e];
-    WSYNC();
-    float b[C::TT][3];
+    // new columns b_p of step t (params off[t] .. off[t+1]-1; at most two chunks)
+    const int p0 = s.off[t], p1 = s.off[t + 1];
 #pragma unroll
     for (int J = 0; J < C::TT; ++J) {
-#pragma unroll
-      for (int st = 0; st < 3; ++st)
-        b[J][st] = (kI[J] <= t) ? s.G[(16 * J + c) * 12 + 4 * st + g] : 0.f;
+      if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
+      const int p = 16 * J + c;
+      if (p >= p0 && p < p1 && g < 3) Gd[J] = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
     }
 #pragma unroll
     for (int I = 0; I < C::TT; ++I) {
       if (kI[I] > t) continue;  // uniform: row block I has no column yet
-      float a[3];
+      float a[4];
 #pragma unroll
-      for (int st = 0; st < 3; ++st) a[st] = q2[st] * b[I][st];
+      for (int q = 0; q < 4; ++q) a[q] = q2[q] * Gd[I][q];
 #pragma unroll
       for (int J = 0; J <= I; ++J) {
         f4 acc = M[tile_index(I, J)];
 #pragma unroll
-        for (int st = 0; st < 3; ++st) acc = mfma4(a[st], b[J][st], acc);
+        for (int q = 0; q < 4; ++q) acc = mfma4(a[q], Gd[J][q], acc);
         M[tile_index(I, J)] = acc;
       }
     }
@@ -298,7 +297,6 @@ __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
       M[tile_index(I, J)] = v;
     }
   }
-  (void)TA;
   WSYNC();
 }
 
