@@ -664,10 +664,12 @@ __device__ __forceinline__ void build_admm_basis(Smem<NC>& s, const KParams& P,
       s.v[p] = 0.f; s.dl[p] = 0.f;
     }
   }
-  for (int k = lane; k <= N; k += 64) {
-    int c = 0;
-    for (int t = 0; t < ntri; ++t) c += ((s.tri[t] >> 2) < k) ? 1 : 0;
-    s.off[k] = 3 * c;
+  {  // off[k] = 3 x (stance (step, leg) pairs before step k): popcount of the stance mask
+    const unsigned long long sm = __ballot(lane < 4 * N && s.tri_of[lane] >= 0);
+    if (lane <= N) {
+      const unsigned long long below = (lane >= 16) ? ~0ull : ((1ull << (4 * lane)) - 1ull);
+      s.off[lane] = 3 * __popcll(sm & below);
+    }
   }
   for (int o = lane; o < 12 * N; o += 64) s.Dt[o] = s.D[o];
   WSYNC();
@@ -740,10 +742,13 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
     s.fpk[lane] = px | (py << 8) | (pz << 16);
   }
   WSYNC();
-  for (int kk = lane; kk <= N; kk += 64) {
-    int c = 0;
-    for (int t = 0; t < ntri; ++t) c += ((s.tri[t] >> 2) < kk) ? s.tcnt[t] : 0;
-    s.off[kk] = c;
+  {  // off[kk] = params of the triples before step kk = the scan base of the first triple of
+     // step >= kk (its index: popcount of the stance mask below step kk), nr past the last
+    const unsigned long long sm = __ballot(lane < 4 * N && s.tri_of[lane] >= 0);
+    const unsigned long long below = (lane >= 16) ? ~0ull : ((1ull << (4 * lane)) - 1ull);
+    const int tstar = __popcll(sm & below);
+    const int bt = __shfl(base, tstar < 64 ? tstar : 63, 64);
+    if (lane <= N) s.off[lane] = (tstar < ntri) ? bt : nr;
   }
   for (int o = lane; o < 12 * N; o += 64) {  // d~ = d + B t0 (LDS only)
     const int kk = o / 12, r = o % 12;
