@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--latency-batch", type=int, default=256)
     ap.add_argument("--dynamics-steps", type=int, default=5,
                     help="timed steps of the on-device dynamics build (+ fused build+solve); 0 = skip")
+    ap.add_argument("--warm-steps", type=int, default=5,
+                    help="timed steps of the warm-started next-tick scenario (+ its cold twin); 0 = skip")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     return ap.parse_args()
@@ -215,6 +217,47 @@ def main():
                             "frac": gbs / HBM_PEAK_GBS, "bytes_per_robot": dyn_bytes // B},
                "fused_build_and_solve_per_s": fused}
 
+    # warm start (centroidal_mpc.py:91-95).  Next-tick proxy: the state
+    # moves (x0 + noise), reference and gait stay; every warm step starts from the previous
+    # tick's (w, y).  Cold and warm solves of the same next-tick batch, same timing method.
+    warm = None
+    if args.warm_steps > 0:
+        y0 = torch.empty((B, 12 * 16), dtype=torch.float32, device=dev)
+        plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"],
+                   out=(w, st, it), stream=stream, y_out=y0)
+        w0 = w.clone()
+        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        sc = torch.tensor([2e-3] * 6 + [2e-2] * 6, device=dev)
+        d2 = dict(d)
+        d2["x0"] = (d["x0"] + torch.randn(d["x0"].shape, generator=g, device=dev) * sc).contiguous()
+        y1 = torch.empty_like(y0)
+
+        def timed(warm_on):
+            for _ in range(2):
+                plan.solve(d2["Ad"], d2["Bd"], d2["gd"], d2["x0"], d2["xref"], d2["contact"],
+                           out=(w, st, it), stream=stream,
+                           **(dict(w_init=w0, y_init=y0, y_out=y1) if warm_on else {}))
+            torch.cuda.synchronize(dev)
+            ta = time.perf_counter()
+            for _ in range(args.warm_steps):
+                plan.solve(d2["Ad"], d2["Bd"], d2["gd"], d2["x0"], d2["xref"], d2["contact"],
+                           out=(w, st, it), stream=stream,
+                           **(dict(w_init=w0, y_init=y0, y_out=y1) if warm_on else {}))
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - ta
+            itn = it.cpu().numpy()
+            return (B * args.warm_steps / el, float(itn.mean()), (st == 1).float().mean().item(),
+                    int(itn.max()), float(np.percentile(itn, 99.9)))
+        cold_rate, cold_it, cold_ok, cold_max, cold_p = timed(False)
+        warm_rate, warm_it, warm_ok, warm_max, warm_p = timed(True)
+        warm = {"scenario": "next tick: x0 + N(0, 2e-3 pos/rpy, 2e-2 vel/omega); warm from the "
+                            "previous tick's (w, y_out), cmpc_solve_warm",
+                "solves_per_s_warm": warm_rate, "solves_per_s_cold": cold_rate,
+                "speedup": warm_rate / cold_rate, "iters_mean_warm": warm_it,
+                "iters_mean_cold": cold_it, "solved_frac_warm": warm_ok,
+                "solved_frac_cold": cold_ok, "iters_max_warm": warm_max,
+                "iters_max_cold": cold_max, "iters_p999_warm": warm_p, "iters_p999_cold": cold_p}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, args.cpu_seconds)
@@ -250,8 +293,10 @@ def main():
             "cpu_baseline": cpu,
             "solved_frac": solved_frac,
             "iters_mean": float(np.mean(iters)),
+            "iters_max": int(np.max(iters)),
             "latency_ms_b256": lat_ms,
             "dynamics": dyn,
+            "warm_start": warm,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},
             "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},

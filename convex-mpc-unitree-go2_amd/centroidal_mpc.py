@@ -99,6 +99,8 @@ class CentroidalMPC:
         self._out = (torch.empty((1, 24 * N), dtype=torch.float32, device=dev),
                      torch.empty((1,), dtype=torch.int32, device=dev),
                      torch.empty((1,), dtype=torch.int32, device=dev))
+        self._y = torch.empty((1, 12 * N), dtype=torch.float32, device=dev)
+        self._warm = False  # no previous solution yet (the reference's x_prev = None)
         self._print_structure()
 
     def _print_structure(self):
@@ -130,8 +132,16 @@ class CentroidalMPC:
             self._buf[k].copy_(torch.as_tensor(v, dtype=self._buf[k].dtype))
         t1 = time.perf_counter()
         b = self._buf
+        # warm start from the previous tick (centroidal_mpc.py:91-95 with OPTS warm_start_primal
+        # / warm_start_dual): the previous w and cmpc's dual, in place on the device
+        kw = {}
+        if self._warm and OPTS["warm_start_primal"]:
+            kw["w_init"] = self._out[0]
+        if self._warm and OPTS["warm_start_dual"]:
+            kw["y_init"] = self._y
         w, st, it = self.plan.solve(b["Ad"], b["Bd"], b["gd"], b["x0"], b["xref"], b["contact"],
-                                    out=self._out)
+                                    out=self._out, y_out=self._y, **kw)
+        self._warm = True
         w_np = w.cpu().numpy()[0].astype(np.float64)
         status = int(st.cpu().item())
         iters = int(it.cpu().item())

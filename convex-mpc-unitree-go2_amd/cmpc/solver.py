@@ -118,11 +118,17 @@ class Plan:
                "cmpc_plan_timing_read")
         return list(ms), list(calls)
 
-    def solve(self, Ad, Bd, gd, x0, xref, contact, out=None, stream=None):
+    def solve(self, Ad, Bd, gd, x0, xref, contact, out=None, stream=None, w_init=None,
+              y_init=None, y_out=None):
         """Solve B instances; all inputs are device tensors (layouts: include/cmpc.h).
 
         Returns (w (B, 24N) fp32, status (B,) int32, iters (B,) int32).  Asynchronous on
-        ``stream`` (default: torch's current stream)."""
+        ``stream`` (default: torch's current stream).
+
+        Warm start (cmpc_solve_warm; the reference's x0 / lam_x0 warm start,
+        centroidal_mpc.py:91-95): ``w_init`` (B, 24N) a previous w, ``y_init`` (B, 12N) a
+        previous dual.  ``y_out`` (B, 12N) receives the dual at the returned forces; pass
+        ``y_out=True`` to allocate it, in which case the return is (w, status, iters, y)."""
         N = self.params.N
         B = Ad.shape[0]
         f32 = torch.float32
@@ -147,11 +153,33 @@ class Plan:
         if stream is None:
             stream = torch.cuda.current_stream(Ad.device)
         sp = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        ret_y = y_out is True
+        if ret_y:
+            y_out = torch.empty((B, 12 * N), dtype=f32, device=Ad.device)
+        if w_init is None and y_init is None and y_out is None:
+            with torch.cuda.device(Ad.device):
+                rc = self.lib.cmpc_solve(self._h, ctypes.c_int64(B),
+                                         *[ctypes.c_void_p(t.data_ptr()) for t in
+                                           (Ad, Bd, gd, x0, xref, contact, w, status, iters)], sp)
+            _check(self.lib, rc, "cmpc_solve")
+            return w, status, iters
+        for t, name, shape in ((w_init, "w_init", (B, 24 * N)), (y_init, "y_init", (B, 12 * N)),
+                               (y_out, "y_out", (B, 12 * N))):
+            if t is not None:
+                _dev_tensor(t, name, f32, shape)
+                if t.device != Ad.device:
+                    raise ValueError("all inputs must be on the same device")
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr() if t is not None else None)
         with torch.cuda.device(Ad.device):
-            rc = self.lib.cmpc_solve(self._h, ctypes.c_int64(B), *[ctypes.c_void_p(t.data_ptr())
-                                     for t in (Ad, Bd, gd, x0, xref, contact, w, status, iters)],
-                                     sp)
-        _check(self.lib, rc, "cmpc_solve")
+            rc = self.lib.cmpc_solve_warm(
+                self._h, ctypes.c_int64(B),
+                *[ptr(t) for t in (Ad, Bd, gd, x0, xref, contact, w_init, y_init, w, y_out,
+                                   status, iters)], sp)
+        _check(self.lib, rc, "cmpc_solve_warm")
+        if ret_y:
+            return w, status, iters, y_out
         return w, status, iters
 
     def build_dynamics(self, mass, inertia, r_feet, xref, dt, out=None, stream=None):

@@ -29,11 +29,14 @@ struct Inputs {
   const float* x0;
   const float* xref;
   const uint8_t* contact;
+  const float* w_init;  // nullable: primal warm start, cmpc_solve_warm's w layout
+  const float* y_init;  // nullable: dual warm start [B][12N] (force layout)
 };
 struct Outputs {
   float* w;
   int32_t* status;
   int32_t* iters;
+  float* y;             // nullable: the dual at the returned forces [B][12N]
 };
 
 // Free-variable capacities of the LDS bins (3 forces per stance (step, leg)).

@@ -206,6 +206,9 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   return CMPC_OK;
 }
 
+static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cmpc::Outputs& out,
+                      void* stream);
+
 int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const float* gd,
                const float* x0, const float* xref, const uint8_t* contact, float* w_out,
                int32_t* status, int32_t* iters, void* stream) {
@@ -215,17 +218,35 @@ int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const
   if (B > pl->p.max_batch) return fail(CMPC_E_RANGE, "cmpc_solve: B exceeds plan max_batch");
   if (!Ad || !Bd || !gd || !x0 || !xref || !contact || !w_out || !status || !iters)
     return fail(CMPC_E_INVALID, "cmpc_solve: null array argument");
+  return solve_impl(pl, B, cmpc::Inputs{Ad, Bd, gd, x0, xref, contact, nullptr, nullptr},
+                    cmpc::Outputs{w_out, status, iters, nullptr}, stream);
+}
+
+int cmpc_solve_warm(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd,
+                    const float* gd, const float* x0, const float* xref,
+                    const uint8_t* contact, const float* w_init, const float* y_init,
+                    float* w_out, float* y_out, int32_t* status, int32_t* iters, void* stream) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_solve_warm: null plan");
+  if (B < 0) return fail(CMPC_E_INVALID, "cmpc_solve_warm: negative batch");
+  if (B == 0) return CMPC_OK;
+  if (B > pl->p.max_batch) return fail(CMPC_E_RANGE, "cmpc_solve_warm: B exceeds plan max_batch");
+  if (!Ad || !Bd || !gd || !x0 || !xref || !contact || !w_out || !status || !iters)
+    return fail(CMPC_E_INVALID, "cmpc_solve_warm: null array argument");
+  return solve_impl(pl, B, cmpc::Inputs{Ad, Bd, gd, x0, xref, contact, w_init, y_init},
+                    cmpc::Outputs{w_out, status, iters, y_out}, stream);
+}
+
+static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cmpc::Outputs& out,
+                      void* stream) {
   hipStream_t st = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(pl->d_counters, 0, 2 * cmpc::kNumBins * sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
   const int threads = 256;
   const unsigned blocks = (unsigned)((B + threads - 1) / threads);
-  hipLaunchKernelGGL(cmpc::bin_kernel, dim3(blocks), dim3(threads), 0, st, pl->kp.N, B, contact,
-                     pl->d_counters, pl->d_lists, pl->p.max_batch);
+  hipLaunchKernelGGL(cmpc::bin_kernel, dim3(blocks), dim3(threads), 0, st, pl->kp.N, B,
+                     in.contact, pl->d_counters, pl->d_lists, pl->p.max_batch);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
-  cmpc::Inputs in{Ad, Bd, gd, x0, xref, contact};
-  cmpc::Outputs out{w_out, status, iters};
   if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   int launched[cmpc::kNumBins] = {0};
   for (int q = 0; q < cmpc::kNumBins; ++q) {

@@ -916,8 +916,52 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   }
   build_admm_basis<NC>(s, P, Bg, ntri);
   const int n = 3 * ntri;
-  for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; s.y[p] = 0.f; }
   s.pcode[lane] = -1;
+  if (in.w_init == nullptr && in.y_init == nullptr) {
+    for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; s.y[p] = 0.f; }
+  } else if (lane < ntri) {
+    // warm start (the reference's x0 / lam_x0 of centroidal_mpc.py:91-95): triple `lane`
+    // (step k, leg l) starts at x = z = Pi_K(u_init), y = y_init; its face code seeds the
+    // polish trigger with the projection of u + y / rho, the first z-update's argument
+    const int kl = s.tri[lane];
+    const int fo = 12 * (kl >> 2) + 3 * (kl & 3);
+    float u[3] = {0.f, 0.f, 0.f}, yv[3] = {0.f, 0.f, 0.f};
+    if (in.w_init) {
+      const float* wi = in.w_init + b * (int64_t)(24 * N) + NP + fo;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) u[a] = wi[a];
+    }
+    if (in.y_init) {
+      const float* yi = in.y_init + b * (int64_t)NP + fo;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) yv[a] = yi[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {  // non-finite warm data falls back to a cold start
+      if (!isfinite(u[a])) u[a] = 0.f;
+      if (!isfinite(yv[a])) yv[a] = 0.f;
+    }
+    float pv[3], qv[3];
+    project(u[0], u[1], u[2], P.mu, P.fz_min, pv[0], pv[1], pv[2]);
+    int code;
+    if (in.y_init) {  // the dual pushes the faces it holds outward
+      const float ir = 1.f / P.rho0;
+      code = project(pv[0] + yv[0] * ir, pv[1] + yv[1] * ir, pv[2] + yv[2] * ir, P.mu, P.fz_min,
+                     qv[0], qv[1], qv[2]);
+    } else {          // primal only: the faces the warm point lies on, to fp32 rounding
+      const float tz = 1e-5f * fmaxf(pv[2], 1.f), lim = P.mu * pv[2] - 1e-5f * pv[2];
+      code = (pv[2] <= P.fz_min + tz) ? 1 : 0;
+      code |= (pv[0] >= lim) ? 2 : (pv[0] <= -lim) ? 4 : 0;
+      code |= (pv[1] >= lim) ? 8 : (pv[1] <= -lim) ? 16 : 0;
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      s.x[3 * lane + a] = pv[a];
+      s.z[3 * lane + a] = pv[a];
+      s.y[3 * lane + a] = yv[a];
+    }
+    s.pcode[lane] = code;
+  }
 
   CMPC_ACC(6, t_inst);
   // ADMM state (x, z, y of triple t at 3t .. 3t+2) lives in LDS, not in registers
@@ -936,6 +980,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   bool parked = false;    // the ADMM inverse is in the park slab
   const float alpha = P.alpha;
   if (n == 0) status = 1;
+  if (n > 0 && in.w_init != nullptr) {
+    // warm active set: the face set of the warm point goes straight to the polish (one
+    // reduced factorization instead of the ADMM one + the polish one); if its KKT check and
+    // repairs fail, ADMM starts from the warm (x, z, y) as above
+    WSYNC();
+    if (lane < ntri) s.code[lane] = s.pcode[lane];
+    nact = polish_setup<NC>(s, P, Bg, ntri);
+    shift = P.sigma;
+    in_polish = true;
+    repairs_left = P.polish_repairs;
+  }
   while (n > 0) {
     if (refactor) {  // the only condense + invert call site
       CMPC_CNT(8, 1);
@@ -982,16 +1037,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         refactor = true;
         continue;
       }
-      // restore the parked ADMM inverse (or rebuild it) and the basis, continue ADMM
-      if (parked) {
-        park_load<NC>(park, M);
-      } else {
-        refactor = true;
-      }
+      // restore the basis and the parked ADMM inverse (or rebuild it first), continue ADMM
       build_admm_basis<NC>(s, P, Bg, ntri);
       in_polish = false;
       nact = n;
       shift = P.sigma + rho;
+      if (parked) {
+        park_load<NC>(park, M);
+      } else {
+        refactor = true;  // M holds the polish inverse: refactor before the next iteration
+        continue;
+      }
     }
     if (it >= P.max_iter) break;
     ++it;
@@ -1114,6 +1170,20 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     wb[NP + o] = uv;
   }
   if (__any(bad)) status = -10;
+  if (out.y) {  // dual at the returned forces, in the force layout (zero on swing legs)
+    if (polished && n > 0) {  // y = -grad f(u*) (the ADMM fixed point); s.g is the reduced one
+      build_admm_basis<NC>(s, P, Bg, ntri);
+      gradient<NC>(s, P, n, s.x, s.g);
+    }
+    const float* yf = polished ? s.g : s.y;
+    const float sg = polished ? -1.f : 1.f;
+    float* yb = out.y + b * (int64_t)NP;
+    for (int o = lane; o < NP; o += 64) {
+      const int k = o / 12, l = (o % 12) / 3, a = o % 3;
+      const int t = s.tri_of[4 * k + l];
+      yb[o] = (t >= 0) ? sg * yf[3 * t + a] : 0.f;
+    }
+  }
   if (lane == 0) {
     out.status[b] = status;
     out.iters[b] = iters;

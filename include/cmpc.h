@@ -94,6 +94,28 @@ int cmpc_solve(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd, con
                const float* x0, const float* xref, const uint8_t* contact, float* w_out,
                int32_t* status, int32_t* iters, void* stream);
 
+/* Warm-started solve: the reference's x0 / lam_x0 / lam_a0 warm start
+ * (centroidal_mpc.py:91-95, kept from the previous solve at :108-110; OPTS warm_start_primal /
+ * warm_start_dual, :33-34).  As cmpc_solve, plus:
+ *   w_init  [B][24N]  fp32  nullable; a previous w_out (optionally shifted by the caller).
+ *                           Only the force part (w_init[b][12N + 12k + 3l + a]) is used: each
+ *                           stance force starts at its projection onto the friction pyramid.
+ *   y_init  [B][12N]  fp32  nullable; a previous y_out (force layout, swing entries ignored).
+ *   y_out   [B][12N]  fp32  nullable; this solver's dual at the returned forces: -grad of the
+ *                           condensed objective at u* (zero on swing legs).  It is cmpc's own
+ *                           multiplier, not OSQP's lam_a (there are no constraint rows here).
+ * With w_init, the faces of the friction pyramid the warm point holds (its forces on a face to
+ * fp32 rounding, or pushed outward by y_init) go straight to the active-set polish: when that
+ * face set (after up to polish_repairs repairs) passes the KKT check, the solve takes one
+ * reduced factorization and no ADMM iteration (iters = 0).  Otherwise ADMM starts from
+ * x = z = the projected warm forces, y = y_init (or 0).
+ * NaN/Inf warm entries start at zero.  w_init may alias w_out and y_init may alias y_out (every
+ * instance reads its warm data before it writes its outputs).  Both NULL == cmpc_solve. */
+int cmpc_solve_warm(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd,
+                    const float* gd, const float* x0, const float* xref,
+                    const uint8_t* contact, const float* w_init, const float* y_init,
+                    float* w_out, float* y_out, int32_t* status, int32_t* iters, void* stream);
+
 void cmpc_plan_destroy(cmpc_plan* plan);
 
 /* QP data on the device: the reference's discrete dynamics

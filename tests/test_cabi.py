@@ -63,6 +63,8 @@ def test_null_arguments(lib):
     assert lib.cmpc_plan_set_timing(None, 1) == -22
     assert lib.cmpc_build_dynamics(None, 1, 0.02, *([None] * 8)) == -22
     assert "cmpc_build_dynamics" in lib.cmpc_last_error().decode()
+    assert lib.cmpc_solve_warm(None, 1, *([None] * 13)) == -22
+    assert "cmpc_solve_warm" in lib.cmpc_last_error().decode()
     lib.cmpc_plan_destroy(None)
 
 

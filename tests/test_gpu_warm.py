@@ -1,0 +1,151 @@
+"""GPU: warm-started solves (cmpc_solve_warm).
+
+The reference warm-starts every tick's OSQP solve with the previous tick's primal and duals
+(centroidal_mpc.py:91-95, stored at :108-110).  The warm start changes where the iteration
+starts, not the answer: every warm-started result is held to the same bar as a cold one
+(U within 1e-4 of the KKT-certified optimum, or of the cold solve of the same problem), and
+must not take more iterations on a problem it has already solved.
+"""
+import numpy as np
+import pytest
+import torch
+
+from parity_util import load_fixture, fixture_batch, rel_err_U, split_w, rollout64, feasibility
+
+pytestmark = pytest.mark.gpu
+TOL_U = 1e-4
+
+
+def _dev(batch, plan):
+    from cmpc.solver import to_device_batch
+    return to_device_batch(batch, plan.device)
+
+
+def _solve(plan, d, **kw):
+    r = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"], **kw)
+    torch.cuda.synchronize(plan.device)
+    return r
+
+
+def test_warm_restart_at_the_optimum(plan):
+    """Warm data = this problem's own solution and dual: the warm face set is the optimal one,
+    so the first (direct) polish succeeds without ADMM iterations, and U is unchanged."""
+    fx = load_fixture("qp_cfg1.npz")
+    d = _dev(fixture_batch(fx), plan)
+    w, st, it, y = _solve(plan, d, y_out=True)
+    assert np.all(st.cpu().numpy() == 1)
+    w2, st2, it2, y2 = _solve(plan, d, w_init=w, y_init=y, y_out=True)
+    st2, it2, it = st2.cpu().numpy(), it2.cpu().numpy(), it.cpu().numpy()
+    assert np.all(st2 == 1), np.unique(st2, return_counts=True)
+    assert rel_err_U(w2.cpu().numpy(), fx["w"]).max() <= TOL_U
+    assert np.all(it2 <= it), (it2.max(), it.max())
+    # the warm face set goes straight to the polish: no ADMM iteration at all
+    assert np.mean(it2 == 0) > 0.99, np.unique(it2, return_counts=True)
+    assert it2.mean() < it.mean()
+    # the returned dual is a fixed point too (same face set, same multipliers); instances whose
+    # optimum is interior have y ~ 0, so the scale is the batch's largest multiplier
+    yn, y2n = y.cpu().numpy(), y2.cpu().numpy()
+    assert np.max(np.abs(y2n - yn)) < 1e-2 * np.abs(yn).max()
+
+
+def _project_pyramid(F, mu, fz_min):
+    """Euclidean projection of (..., 3) forces onto {|fx|, |fy| <= mu fz, fz >= fz_min}
+    (float64; the same case split as the solver's z-update)."""
+    a, b, c = F[..., 0], F[..., 1], F[..., 2]
+    A, Bb = np.abs(a), np.abs(b)
+    lo, hi = np.minimum(A, Bb), np.maximum(A, Bb)
+    z1 = (c + mu * (A + Bb)) / (1 + 2 * mu * mu)
+    z2 = (c + mu * hi) / (1 + mu * mu)
+    z = np.where(mu * z1 < lo, z1, np.where(mu * z2 < hi, z2, c))
+    z = np.maximum(z, fz_min)
+    lim = mu * z
+    return np.stack([np.clip(a, -lim, lim), np.clip(b, -lim, lim), z], axis=-1)
+
+
+def test_dual_out_is_a_kkt_multiplier(plan):
+    """y_out: zero on swing legs; on stance legs y lies in the normal cone of the friction
+    pyramid at u -- moving u along y and projecting back returns u (complementarity)."""
+    from cmpc import synth
+    b = synth.make_config(2, B=512)
+    d = _dev(b, plan)
+    w, st, it, y = _solve(plan, d, y_out=True)
+    ok = st.cpu().numpy() == 1
+    assert ok.mean() > 0.99
+    _, U = split_w(w.cpu().numpy().astype(np.float64))
+    Y = y.cpu().numpy().astype(np.float64)
+    F = U.reshape(len(U), 16, 4, 3)
+    L = Y.reshape(len(U), 16, 4, 3)
+    ct = b["contact"].transpose(0, 2, 1).astype(bool)          # (B, N, 4)
+    assert np.all(L[~ct] == 0)
+    fmax = np.abs(U).reshape(len(U), -1).max(1)
+    lmax = np.abs(Y).max()  # batch scale: an interior optimum has y ~ 0 (rounding only)
+    t = (0.1 * fmax / lmax)[:, None, None, None]
+    P = _project_pyramid(F + t * L, plan.params.mu, plan.params.fz_min)
+    dev = np.where(ct[..., None], np.abs(P - F), 0.0).reshape(len(U), -1).max(1) / fmax
+    assert dev[ok].max() < 1e-3, (dev[ok].max(), int(np.flatnonzero(ok)[dev[ok].argmax()]))
+
+
+def test_warm_next_tick(plan):
+    """Closed-loop proxy: the next tick's problem (state moved, same reference and gait) warm-
+    started from this tick's (w, y), as centroidal_mpc.py:91-95 does without shifting.  Same
+    answer as the cold solve of the new problem, in fewer iterations on average."""
+    from cmpc import synth
+    b = synth.make_config(2, B=4096)
+    d = _dev(b, plan)
+    w, st, it, y = _solve(plan, d, y_out=True)
+    rng = np.random.default_rng(5)
+    b2 = dict(b)
+    b2["x0"] = b["x0"] + rng.normal(scale=[2e-3] * 6 + [2e-2] * 6, size=b["x0"].shape)
+    d2 = _dev(b2, plan)
+    wc, stc, itc = _solve(plan, d2)
+    ww, stw, itw, yw = _solve(plan, d2, w_init=w, y_init=y, y_out=True)
+    stc, stw = stc.cpu().numpy(), stw.cpu().numpy()
+    itc, itw = itc.cpu().numpy(), itw.cpu().numpy()
+    assert np.mean(stw == 1) >= np.mean(stc == 1) - 1e-3
+    both = (stc == 1) & (stw == 1)
+    assert both.mean() > 0.99
+    err = rel_err_U(ww.cpu().numpy()[both], wc.cpu().numpy()[both])
+    assert err.max() <= 2 * TOL_U, (err.max(), int(np.flatnonzero(both)[err.argmax()]))
+    assert itw.mean() < itc.mean(), (itw.mean(), itc.mean())
+    assert np.mean(itw == 0) > 0.95, np.unique(itw, return_counts=True)
+    Xg, Ug = split_w(ww.cpu().numpy().astype(np.float64))
+    assert feasibility(b2, Ug).max() < 1e-2
+    assert np.max(np.abs(Xg - rollout64(b2, Ug))) < 1e-3
+    # certified optimum on a few instances
+    from oracle import mpc_qp, tight_solver
+    for i in (0, 1, 2, 3, 1000, 2047):
+        qp = mpc_qp.build_qp(b2["Ad"][i], b2["Bd"][i], b2["gd"][i], b2["x0"][i],
+                             b2["xref"][i].T, b2["contact"][i])
+        r = tight_solver.solve(qp)
+        assert rel_err_U(ww[i:i + 1].cpu().numpy(), r["w"][None])[0] <= TOL_U
+
+
+def test_warm_garbage_and_aliasing(plan):
+    """Non-finite / huge warm data and in-place warm buffers (w_init is w_out, y_init is
+    y_out) still give the certified answer."""
+    fx = load_fixture("qp_cfg1.npz")
+    d = _dev(fixture_batch(fx), plan)
+    B = d["Ad"].shape[0]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    w = (torch.randn((B, 24 * 16), generator=g) * 1e3).to(plan.device)
+    y = (torch.randn((B, 12 * 16), generator=g) * 1e2).to(plan.device)
+    w[::7] = float("nan")
+    y[::5] = float("inf")
+    st = torch.empty((B,), dtype=torch.int32, device=plan.device)
+    it = torch.empty_like(st)
+    _solve(plan, d, out=(w, st, it), w_init=w, y_init=y, y_out=y)
+    stn = st.cpu().numpy()
+    assert np.mean(stn == 1) > 0.99, np.unique(stn, return_counts=True)
+    ok = stn == 1
+    assert rel_err_U(w.cpu().numpy()[ok], fx["w"][ok]).max() <= TOL_U
+    assert torch.isfinite(y).all()
+
+
+def test_warm_primal_only_and_dual_only(plan):
+    fx = load_fixture("qp_cfg1.npz")
+    d = _dev(fixture_batch(fx), plan)
+    w, st, it, y = _solve(plan, d, y_out=True)
+    for kw in (dict(w_init=w), dict(y_init=y)):
+        w2, st2, it2 = _solve(plan, d, **kw)
+        assert np.all(st2.cpu().numpy() == 1)
+        assert rel_err_U(w2.cpu().numpy(), fx["w"]).max() <= TOL_U

@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--config", type=int, default=1)
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--lib", default=str(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_stamps.so"))
+    ap.add_argument("--warm", action="store_true",
+                    help="measure the bench's next-tick warm-start scenario (cold twin first)")
     ap.add_argument("--only-bin", type=int, default=-1, help="keep only instances of this bin (0-3)")
     a = ap.parse_args()
     import torch
@@ -36,10 +38,26 @@ def main():
     d = to_device_batch(b)
     plan = Plan(SolverParams(max_batch=a.batch))
     buf = (ctypes.c_ulonglong * 16)()
-    plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+    kw = {}
+    if a.warm:
+        y0 = torch.empty((a.batch, 12 * 16), dtype=torch.float32, device=d["Ad"].device)
+        w0, _, _ = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"], y_out=y0)
+        g = torch.Generator(device=d["Ad"].device).manual_seed(1234)
+        sc = torch.tensor([2e-3] * 6 + [2e-2] * 6, device=d["Ad"].device)
+        d["x0"] = (d["x0"] + torch.randn(d["x0"].shape, generator=g, device=d["Ad"].device) * sc).contiguous()
+        torch.cuda.synchronize()
+        report(lib, plan, d, buf, {}, "cold (next tick)")
+        kw = dict(w_init=w0, y_init=y0, y_out=torch.empty_like(y0))
+    report(lib, plan, d, buf, kw, "warm (next tick)" if a.warm else "cold")
+
+
+def report(lib, plan, d, buf, kw, title):
+    import torch
+    plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"], **kw)
     torch.cuda.synchronize()
     lib.cmpc_debug_stamps(buf)
-    w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+    r = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"], **kw)
+    st = r[1]
     torch.cuda.synchronize()
     lib.cmpc_debug_stamps(buf)
     v = np.array(list(buf), dtype=np.float64)
@@ -47,6 +65,7 @@ def main():
     names = ["condense", "invert", "gradient", "symv", "polish(all, incl. grad/symv)",
              "instance total", "setup", "admm rest", None, None, None, None, None, None,
              "polish setup", "output"]
+    print(f"== {title}")
     print(f"instances {int(n)}  mean iters {v[11]/n:.2f}  condense_invert/inst {v[8]/n:.2f}  "
           f"polish attempts/inst {v[9]/n:.2f}")
     for i, nm in enumerate(names):
@@ -55,7 +74,6 @@ def main():
         print(f"  {nm:28s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
     print(f"  per call: condense {v[0]/v[8]:.0f}  invert {v[1]/v[8]:.0f}  gradient {v[2]/max(v[12],1):.0f} (x{v[12]/n:.1f})  symv {v[3]/max(v[13],1):.0f} (x{v[13]/n:.1f}) cycles")
     print("  status:", dict(zip(*np.unique(st.cpu().numpy(), return_counts=True))))
-
 
 if __name__ == "__main__":
     main()
