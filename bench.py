@@ -73,6 +73,9 @@ def parse():
                     help="timed steps of the on-device dynamics build (+ fused build+solve); 0 = skip")
     ap.add_argument("--warm-steps", type=int, default=5,
                     help="timed steps of the warm-started next-tick scenario (+ its cold twin); 0 = skip")
+    ap.add_argument("--tick-steps", type=int, default=5,
+                    help="timed steps of the all-on-device MPC tick (generate_traj -> "
+                         "build_dynamics -> solve); 0 = skip")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     return ap.parse_args()
@@ -258,6 +261,63 @@ def main():
                 "solved_frac_cold": cold_ok, "iters_max_warm": warm_max,
                 "iters_max_cold": cold_max, "iters_p999_warm": warm_p, "iters_p999_cold": cold_p}
 
+    # the whole tick on the device -- reference trajectory, contact table
+    # and foot levers (cmpc_generate_traj, com_trajectory.py:27-207) -> discrete dynamics -> solve.
+    # Inputs are what ComTraj.generate_traj reads from the robot (state, command, time, gait,
+    # current levers); the traj kernel gets its own HBM roofline.
+    tick = None
+    if args.tick_steps > 0:
+        tk = synth.make_tick_inputs(B, seed=synth.CONFIGS[min(cfg, 2)]["seed"] + 500 + 1000 * rank,
+                                    mixed=cfg != 1)
+        f32, f64 = torch.float32, torch.float64
+        td = {k: torch.as_tensor(tk[k], dtype=f64 if k in ("pos_des", "t_now", "gait") else f32)
+              .contiguous().to(dev) for k in ("x0", "pos_des", "cmd", "t_now", "gait", "foot_lever",
+                                              "hip", "m", "I_world")}
+        dtt = float(tk["dt"])
+        pd0 = td["pos_des"].clone()
+        N = 16
+        touts = (torch.empty((B, N, 12), dtype=f32, device=dev),
+                 torch.empty((B, 4, N), dtype=torch.uint8, device=dev),
+                 torch.empty((B, N, 4, 3), dtype=f32, device=dev))
+        douts = (torch.empty_like(d["Ad"]), torch.empty_like(d["Bd"]), torch.empty_like(d["gd"]))
+
+        def gen():
+            plan.generate_traj(td["x0"], td["pos_des"], td["cmd"], td["t_now"], td["gait"],
+                               td["foot_lever"], td["hip"], dtt, out=touts, stream=stream)
+
+        def full_tick():
+            gen()
+            plan.build_dynamics(td["m"], td["I_world"], touts[2], touts[0], dtt, out=douts,
+                                stream=stream)
+            plan.solve(douts[0], douts[1], douts[2], td["x0"], touts[0], touts[1],
+                       out=(w, st, it), stream=stream)
+        for _ in range(2):
+            full_tick()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.tick_steps):
+            gen()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        tr_ms = e0.elapsed_time(e1) / args.tick_steps
+        tr_bytes = 48 + 24 + 16 + 8 + 48 + 48 + N * 48 + 4 * N + N * 48 + 24   # in + out per robot
+        t0t = time.perf_counter()
+        for _ in range(args.tick_steps):
+            full_tick()
+        torch.cuda.synchronize(dev)
+        tick_rate = B * args.tick_steps / (time.perf_counter() - t0t)
+        td["pos_des"].copy_(pd0)
+        tick_it = it.cpu().numpy()
+        gbs_t = tr_bytes * B / (tr_ms * 1e-3) / 1e9
+        tick = {"kernel": "traj_kernel", "ms_per_step": tr_ms,
+                "roofline": {"bound": "hbm", "achieved": gbs_t, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": gbs_t / HBM_PEAK_GBS, "bytes_per_robot": tr_bytes},
+                "full_tick_per_s": tick_rate,
+                "full_tick": "generate_traj + build_dynamics + cold solve, all on the device",
+                "solved_frac": float((st == 1).float().mean().item()),
+                "iters_mean": float(tick_it.mean())}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, args.cpu_seconds)
@@ -297,6 +357,7 @@ def main():
             "latency_ms_b256": lat_ms,
             "dynamics": dyn,
             "warm_start": warm,
+            "tick": tick,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},
             "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},

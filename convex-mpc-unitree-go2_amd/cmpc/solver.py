@@ -218,6 +218,50 @@ class Plan:
         return Ad, Bd, gd
 
 
+    def generate_traj(self, x0, pos_des, cmd, t_now, gait, foot_lever, hip, dt, out=None,
+                      stream=None):
+        """Reference trajectory, contact table and foot levers of B robots on the device -- the
+        reference's ComTraj.generate_traj (com_trajectory.py:27-207) up to the dynamics
+        (cmpc_generate_traj, include/cmpc.h).  x0 (B,12) fp32; pos_des (B,3) fp64, updated in
+        place (ComTraj.pos_des_world); cmd (B,4) fp32 [vx_body, vy_body, z_des, yaw_rate];
+        t_now (B,) fp64; gait (B,6) fp64 [period, duty, 4 phase offsets]; foot_lever (B,4,3)
+        fp32; hip (4,3) fp32.  Returns (xref (B,N,12), contact (B,4,N) uint8,
+        r_feet (B,N,4,3))."""
+        N = self.params.N
+        B = x0.shape[0]
+        f32, f64 = torch.float32, torch.float64
+        _dev_tensor(x0, "x0", f32, (B, 12))
+        _dev_tensor(pos_des, "pos_des", f64, (B, 3))
+        _dev_tensor(cmd, "cmd", f32, (B, 4))
+        _dev_tensor(t_now, "t_now", f64, (B,))
+        _dev_tensor(gait, "gait", f64, (B, 6))
+        _dev_tensor(foot_lever, "foot_lever", f32, (B, 4, 3))
+        _dev_tensor(hip, "hip", f32, (4, 3))
+        for t in (pos_des, cmd, t_now, gait, foot_lever, hip):
+            if t.device != x0.device:
+                raise ValueError("all inputs must be on the same device")
+        if out is None:
+            xref = torch.empty((B, N, 12), dtype=f32, device=x0.device)
+            contact = torch.empty((B, 4, N), dtype=torch.uint8, device=x0.device)
+            r_feet = torch.empty((B, N, 4, 3), dtype=f32, device=x0.device)
+        else:
+            xref, contact, r_feet = out
+            _dev_tensor(xref, "xref", f32, (B, N, 12))
+            _dev_tensor(contact, "contact", torch.uint8, (B, 4, N))
+            _dev_tensor(r_feet, "r_feet", f32, (B, N, 4, 3))
+        if stream is None:
+            stream = torch.cuda.current_stream(x0.device)
+        sp = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        with torch.cuda.device(x0.device):
+            rc = self.lib.cmpc_generate_traj(
+                self._h, ctypes.c_int64(B), ctypes.c_double(dt),
+                *[ctypes.c_void_p(t.data_ptr()) for t in (x0, pos_des, cmd, t_now, gait,
+                                                          foot_lever, hip, xref, contact, r_feet)],
+                sp)
+        _check(self.lib, rc, "cmpc_generate_traj")
+        return xref, contact, r_feet
+
+
 def to_device_batch(batch: dict, device="cuda") -> dict:
     """float64/uint8 numpy batch (cmpc.synth layout) -> contiguous device tensors."""
     out = {}

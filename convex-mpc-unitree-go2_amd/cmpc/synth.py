@@ -146,6 +146,49 @@ def make_batch(B: int, seed: int, mixed: bool = False, N: int = N_HORIZON, dt: f
                 m=m, I_world=I_world, r_legs=r_legs, yaw_avg=yaw_avg, dt=dt, N=N)
 
 
+HIP_OFFSETS = np.concatenate([HIP_XY, np.zeros((4, 1))], axis=1)   # body frame, legs FL FR RL RR
+
+
+def make_tick_inputs(B: int, seed: int, mixed: bool = False, N: int = N_HORIZON,
+                     gait_hz: float = GAIT_HZ):
+    """Per-robot inputs of one MPC tick before ``ComTraj.generate_traj`` (com_trajectory.py:27-35):
+    the state, the persistent desired position, the command, the time, the gait and the current
+    foot levers -- what ``cmpc_generate_traj`` consumes (include/cmpc.h).  Same state / command
+    distribution as :func:`make_batch`; mixed=True draws per-robot phase offsets U(0,1)^4 and
+    duty U(0.4,0.8).  fp32-representable where the boundary is fp32."""
+    rng = np.random.default_rng(seed)
+    f32 = lambda a: np.asarray(a, np.float32).astype(np.float64)   # noqa: E731
+    yaw = rng.uniform(-np.pi, np.pi, B)
+    vx, vy, wz = rng.uniform(-0.8, 0.8, B), rng.uniform(-0.4, 0.4, B), rng.uniform(-4.0, 4.0, B)
+    Rz = _rz(yaw)
+    v_des = np.einsum('bij,bj->bi', Rz, np.stack([vx, vy, np.zeros(B)], -1))
+    x0 = np.zeros((B, 12))
+    x0[:, 0:2] = rng.uniform(-1, 1, (B, 2))
+    x0[:, 2] = rng.normal(0.27, 0.01, B)
+    x0[:, 3:5] = rng.normal(0, 0.05, (B, 2))
+    x0[:, 5] = yaw
+    x0[:, 6:9] = v_des + rng.normal(0, 0.1, (B, 3))
+    x0[:, 9:11] = rng.normal(0, 0.2, (B, 2))
+    x0[:, 11] = wz
+    x0 = f32(x0)
+    pos_des = x0[:, 0:3] + np.concatenate([rng.uniform(-0.15, 0.15, (B, 2)),
+                                           np.zeros((B, 1))], axis=1)
+    cmd = f32(np.stack([vx, vy, np.full(B, Z_DES), wz], -1))
+    period = 1.0 / gait_hz
+    if mixed:
+        gait = np.concatenate([np.full((B, 1), period), rng.uniform(0.4, 0.8, (B, 1)),
+                               rng.uniform(0, 1, (B, 4))], axis=1)
+    else:
+        gait = np.tile(np.array([period, GAIT_DUTY, *TROT_OFFSETS]), (B, 1))
+    t_now = rng.uniform(0.0, 10.0, B)
+    hip_w = np.einsum('bij,lj->bli', Rz[:, :2, :2], HIP_XY)
+    foot_lever = f32(np.concatenate([hip_w, (-Z_DES + rng.normal(0, 0.01, (B, 4)))[..., None]], -1))
+    m = np.full(B, MASS)
+    I_world = np.einsum('bij,jk,blk->bil', Rz, INERTIA_BODY, Rz)
+    return dict(x0=x0, pos_des=pos_des, cmd=cmd, t_now=t_now, gait=gait, foot_lever=foot_lever,
+                hip=f32(HIP_OFFSETS), m=m, I_world=I_world, dt=period / N, N=N)
+
+
 CONFIGS = {
     0: dict(B=1, seed=0, mixed=False),
     1: dict(B=256, seed=1, mixed=False),

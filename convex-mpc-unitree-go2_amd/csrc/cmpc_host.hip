@@ -14,6 +14,7 @@
 
 #include "cmpc_wave.hip"      // solve kernels: same translation unit
 #include "cmpc_dynamics.hip"  // QP-data (discrete dynamics) kernel
+#include "cmpc_traj.hip"      // reference trajectory / contact table / foot levers kernel
 
 struct cmpc_plan {
   cmpc_params p;
@@ -304,6 +305,26 @@ int cmpc_build_dynamics(cmpc_plan* pl, int64_t B, float dt, const float* mass,
                      Bd, gd);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "dynamics_kernel launch");
+  return CMPC_OK;
+}
+
+int cmpc_generate_traj(cmpc_plan* pl, int64_t B, double dt, const float* x0, double* pos_des,
+                       const float* cmd, const double* t_now, const double* gait,
+                       const float* foot_lever, const float* hip, float* xref, uint8_t* contact,
+                       float* r_feet, void* stream) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_generate_traj: null plan");
+  if (B < 0) return fail(CMPC_E_INVALID, "cmpc_generate_traj: negative batch");
+  if (!(dt > 0.0) || !std::isfinite(dt)) return fail(CMPC_E_INVALID, "cmpc_generate_traj: dt must be > 0");
+  if (B == 0) return CMPC_OK;
+  if (!x0 || !pos_des || !cmd || !t_now || !gait || !foot_lever || !hip || !xref || !contact ||
+      !r_feet)
+    return fail(CMPC_E_INVALID, "cmpc_generate_traj: null array argument");
+  const long long blocks = B < 8192 ? B : 8192;  // grid-stride, one wave per robot
+  hipLaunchKernelGGL(cmpc::traj_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
+                     pl->kp.N, dt, B, x0, pos_des, cmd, t_now, gait, foot_lever, hip, xref,
+                     contact, r_feet);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "traj_kernel launch");
   return CMPC_OK;
 }
 

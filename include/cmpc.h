@@ -136,6 +136,33 @@ int cmpc_build_dynamics(cmpc_plan* plan, int64_t B, float dt, const float* mass,
                         const float* inertia, const float* r_feet, const float* xref,
                         float* Ad, float* Bd, float* gd, void* stream);
 
+/* Reference trajectory, contact table and foot levers on the device: the
+ * reference's ComTraj.generate_traj (com_trajectory.py:27-207) up to the dynamics, for B robots,
+ * with the Pinocchio quantities it reads passed in (see oracle/traj_ref.py):
+ *   x0         [B][12]    fp32   go2.compute_com_x_vec() (com_trajectory.py:37): p, rpy, v, w.
+ *                                R_z(x0[5]) is go2.R_z; (R_z R_y R_x)(x0[3:6])' is
+ *                                go2.R_world_to_body (go2_robot_data.py:211-222)
+ *   pos_des    [B][3]     fp64   in/out: ComTraj.pos_des_world, the per-robot desired position
+ *                                (initialise to x0[0:3], com_trajectory.py:12-13); clamped to
+ *                                0.1 m of x0 in x/y and set to the commanded z (:47-60)
+ *   cmd        [B][4]     fp32   x_vel_des_body, y_vel_des_body, z_pos_des_body,
+ *                                yaw_rate_des_body (generate_traj's arguments, :27-35)
+ *   t_now      [B]        fp64   time_now (:30)
+ *   gait       [B][6]     fp64   gait_period (= 1/frequency_hz), duty, phase offsets FL FR RL RR
+ *                                (gait.py:8, 13-19)
+ *   foot_lever [B][4][3]  fp32   go2.get_foot_lever_world() (:113, go2_robot_data.py:261-269)
+ *   hip        [4][3]     fp32   go2.get_hip_offset(leg), body frame (gait.py:46), all robots
+ *   xref       [B][N][12] fp32   out: compute_x_ref_vec() transposed (cmpc_solve's layout)
+ *   contact    [B][4][N]  uint8  out: contact_table (:106, gait.py:26-37), bit-identical
+ *   r_feet     [B][N][4][3] fp32 out: r_{fl,fr,rl,rr}_foot_world (:108-207), the levers
+ *                                cmpc_build_dynamics takes
+ * N is the plan's horizon (the reference's int(gait_period / time_step)); dt = time_step > 0.
+ * Asynchronous on `stream`; the outputs chain into cmpc_build_dynamics and cmpc_solve. */
+int cmpc_generate_traj(cmpc_plan* plan, int64_t B, double dt, const float* x0, double* pos_des,
+                       const float* cmd, const double* t_now, const double* gait,
+                       const float* foot_lever, const float* hip, float* xref, uint8_t* contact,
+                       float* r_feet, void* stream);
+
 /* Measurement hooks (not on the reference's interface; used by bench.py).  While enabled,
  * cmpc_solve records a hipEvent pair around every solve-kernel launch (one per free-variable
  * bin; the bins run concurrently on plan-internal streams joined back to `stream`).  cmpc_plan_timing_read waits for the recorded events, returns the

@@ -7,7 +7,14 @@
    Pinocchio-backed robot model replaced by a synthetic stand-in object (no URDF exists in the
    image; only its outputs m, I_com, foot levers feed the QP).  Pins oracle/mpc_qp.py and
    cmpc/synth.py's discretisation.
-2. ``qp_cfg1.npz`` / ``qp_cfg2.npz`` -- synthetic batches (cmpc.synth, SURVEY.md 8(d) configs
+2. ``traj_ticks.npz`` -- consecutive MPC ticks of ``ComTraj.generate_traj`` (com_trajectory.py:
+   27-207: desired-position clamp, x_ref, contact table, foot levers with touchdown prediction,
+   gait.py:21-74) for robots with random gaits (``gait.PHASE_OFFSET`` set per robot), run by the
+   reference's own code on a stand-in robot whose base rotation is the full ZYX rotation of its
+   state (scipy ``Rotation``).  Inputs are fp32-representable (the C-ABI's boundary type) except
+   time and gait, which the C-ABI takes in float64.  Pins oracle/traj_ref.py and
+   ``cmpc_generate_traj``.
+3. ``qp_cfg1.npz`` / ``qp_cfg2.npz`` -- synthetic batches (cmpc.synth, SURVEY.md 8(d) configs
    1 and 2) with their KKT-certified float64 optimum from oracle/tight_solver.py, in the
    reference layout (w, lam_x, lam_a) plus the certificate residuals.
 
@@ -75,6 +82,20 @@ class SyntheticGo2:
         self.R_z = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1.0]])
 
 
+class SyntheticGo2Full(SyntheticGo2):
+    """As SyntheticGo2, but ``R_world_to_body`` is the full base rotation R_z R_y R_x of the
+    state's roll/pitch/yaw (what Pinocchio's oMb.rotation is for that state,
+    go2_robot_data.py:211-216), computed independently of the oracle with scipy."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        from scipy.spatial.transform import Rotation
+        r, p, y = self._x0[3:6]
+        R = Rotation.from_euler("ZYX", [y, p, r]).as_matrix()
+        self.R_body_to_world = R
+        self.R_world_to_body = R.T
+
+
 def import_reference():
     """Import gait.py / com_trajectory.py from the reference (pure NumPy/SciPy).  Their module
     header imports ``go2_robot_data`` (Pinocchio); that module is replaced by a namespace whose
@@ -126,6 +147,67 @@ def make_ref_inputs(n_cases: int = 6):
     print("ref_inputs.npz:", n_cases, "cases")
 
 
+def _f32(x):
+    return np.asarray(np.float32(x), dtype=np.float64)
+
+
+def make_traj_ticks(n_robots: int = 10, n_ticks: int = 6):
+    """Consecutive ticks of the reference's generate_traj, per robot (see module doc)."""
+    gait_mod, ct_mod = import_reference()
+    rng = np.random.default_rng(11)
+    hip = _f32(np.array([[0.1934, 0.0465, 0.0], [0.1934, -0.0465, 0.0],
+                         [-0.1934, 0.0465, 0.0], [-0.1934, -0.0465, 0.0]])
+               + np.array([[0, 0.0955, 0], [0, -0.0955, 0], [0, 0.0955, 0], [0, -0.0955, 0]]))
+    rec = {k: [] for k in ("x0", "pos_des_in", "pos_des_out", "cmd", "t_now", "gait", "N", "dt",
+                           "foot_lever", "xref", "contact", "r_feet")}
+    for r in range(n_robots):
+        hz = [3.0, 2.0, 3.0, 4.0, 2.5][r % 5]
+        duty = [0.6, 0.5, 0.75, 0.4, 0.62][r % 5]
+        offs = np.array([0.5, 0.0, 0.0, 0.5]) if r % 2 == 0 else rng.uniform(0, 1, 4)
+        div = 8 if r == n_robots - 1 else 16          # one N = 8 robot
+        g = gait_mod.Gait(hz, duty)
+        dt = g.gait_period / div
+        t_now = float(rng.uniform(0, 2.0))
+        x0 = _f32(np.array([rng.uniform(-1, 1), rng.uniform(-1, 1), 0.27 + 0.01 * rng.normal(),
+                            0.05 * rng.normal(), 0.05 * rng.normal(), rng.uniform(-np.pi, np.pi),
+                            0.3 * rng.normal(), 0.3 * rng.normal(), 0.05 * rng.normal(),
+                            0.1 * rng.normal(), 0.1 * rng.normal(), 0.5 * rng.normal()]))
+        go2 = SyntheticGo2Full(x0=x0, feet=[np.zeros(3)] * 4)
+        traj = ct_mod.ComTraj(go2)
+        # the touchdown prediction reads the hip offsets of ComTraj's dummy model (:139)
+        traj.dummy_go2._hip = {n: hip[i].copy() for i, n in enumerate(("FL", "FR", "RL", "RR"))}
+        for t in range(n_ticks):
+            cmd = _f32([rng.uniform(-0.8, 0.8), rng.uniform(-0.4, 0.4), 0.27 + 0.02 * rng.normal(),
+                        rng.uniform(-3, 3)])
+            feet = [_f32(hip[i] + np.array([0, 0, -0.27]) + 0.02 * rng.normal(size=3))
+                    for i in range(4)]
+            go2 = SyntheticGo2Full(x0=x0, feet=feet, hip=hip[:, :2])
+            go2._hip = {n: hip[i].copy() for i, n in enumerate(("FL", "FR", "RL", "RR"))}
+            gait_mod.PHASE_OFFSET = offs.copy()
+            pd_in = np.array(traj.pos_des_world, dtype=np.float64, copy=True)
+            traj.generate_traj(go2, g, t_now, cmd[0], cmd[1], cmd[2], cmd[3], time_step=dt)
+            assert traj.N == div, (traj.N, div)
+            r_feet = np.zeros((16, 4, 3))
+            r_feet[:div] = np.stack([traj.r_fl_foot_world, traj.r_fr_foot_world,
+                                     traj.r_rl_foot_world, traj.r_rr_foot_world], 0).transpose(2, 0, 1)
+            xref = np.zeros((16, 12)); xref[:div] = traj.compute_x_ref_vec().T
+            ct = np.zeros((4, 16), np.uint8); ct[:, :div] = traj.contact_table
+            for k, v in (("x0", x0), ("pos_des_in", pd_in), ("pos_des_out", traj.pos_des_world),
+                         ("cmd", cmd), ("t_now", t_now),
+                         ("gait", [g.gait_period, duty, *offs]), ("N", div), ("dt", dt),
+                         ("foot_lever", np.stack(feet)), ("xref", xref), ("contact", ct),
+                         ("r_feet", r_feet)):
+                rec[k].append(np.array(v, copy=True))
+            # next tick: time advances one MPC step, the state moves a little
+            t_now += dt
+            x0 = _f32(x0 + np.concatenate([x0[6:9] * dt, x0[9:12] * dt, 0.05 * rng.normal(size=6)]))
+    gait_mod.PHASE_OFFSET = np.array([0.5, 0.0, 0.0, 0.5])
+    out = {k: np.stack(v) for k, v in rec.items()}
+    out["hip"] = hip
+    np.savez_compressed(HERE / "traj_ticks.npz", **out)
+    print("traj_ticks.npz:", len(rec["N"]), "ticks")
+
+
 def make_qp_fixture(cfg: int, B: int, name: str):
     b = synth.make_config(cfg, B=B)
     W, LX, LA, KKT = [], [], [], []
@@ -146,5 +228,6 @@ def make_qp_fixture(cfg: int, B: int, name: str):
 
 if __name__ == "__main__":
     make_ref_inputs()
+    make_traj_ticks()
     make_qp_fixture(1, 32, "qp_cfg1.npz")
     make_qp_fixture(2, 64, "qp_cfg2.npz")

@@ -65,6 +65,8 @@ def test_null_arguments(lib):
     assert "cmpc_build_dynamics" in lib.cmpc_last_error().decode()
     assert lib.cmpc_solve_warm(None, 1, *([None] * 13)) == -22
     assert "cmpc_solve_warm" in lib.cmpc_last_error().decode()
+    assert lib.cmpc_generate_traj(None, 1, 0.02, *([None] * 11)) == -22
+    assert "cmpc_generate_traj" in lib.cmpc_last_error().decode()
     lib.cmpc_plan_destroy(None)
 
 
