@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--tick-steps", type=int, default=5,
                     help="timed steps of the all-on-device MPC tick (generate_traj -> "
                          "build_dynamics -> solve); 0 = skip")
+    ap.add_argument("--param", action="append", default=[],
+                    help="SolverParams override key=value (experiments)")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     return ap.parse_args()
@@ -115,7 +117,11 @@ def main():
                                  mixed=synth.CONFIGS[cfg]["mixed"])
     bins = bins_of(batch["contact"])
     d = to_device_batch(batch, dev)
-    plan = Plan(SolverParams(max_batch=B), device=dev)
+    over = {}
+    for kv in args.param:
+        k, v = kv.split("=")
+        over[k] = type(getattr(SolverParams, k))(float(v) if "." in v or "e" in v else int(v))
+    plan = Plan(SolverParams(max_batch=B, **over), device=dev)
     w = torch.empty((B, 24 * 16), dtype=torch.float32, device=dev)
     st = torch.empty((B,), dtype=torch.int32, device=dev)
     it = torch.empty((B,), dtype=torch.int32, device=dev)
@@ -358,6 +364,7 @@ def main():
             "dynamics": dyn,
             "warm_start": warm,
             "tick": tick,
+            "params_override": over or None,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},
             "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},

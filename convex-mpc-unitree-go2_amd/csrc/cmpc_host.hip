@@ -251,9 +251,7 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   int launched[cmpc::kNumBins] = {0};
   for (int q = 0; q < cmpc::kNumBins; ++q) {
-    const int cap = cmpc::kBinCap[q];
-    if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) break;  // bins beyond 12N are empty
-    (void)cap;
+    if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) continue;  // bins beyond 12N are empty
     const long long g = pl->grid[q] < B ? pl->grid[q] : B;
     hipStream_t bs = pl->bin_stream[q];
     if ((e = hipStreamWaitEvent(bs, pl->fork, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
@@ -299,7 +297,11 @@ int cmpc_build_dynamics(cmpc_plan* pl, int64_t B, float dt, const float* mass,
   if (B == 0) return CMPC_OK;
   if (!mass || !inertia || !r_feet || !xref || !Ad || !Bd || !gd)
     return fail(CMPC_E_INVALID, "cmpc_build_dynamics: null array argument");
-  const long long blocks = B < 8192 ? B : 8192;  // grid-stride: ~32 resident waves per CU
+#ifndef CMPC_DYN_GRID_CAP
+#define CMPC_DYN_GRID_CAP 8192
+#endif
+  const long long cap = CMPC_DYN_GRID_CAP;
+  const long long blocks = B < cap ? B : cap;  // grid-stride: ~32 resident waves per CU
   hipLaunchKernelGGL(cmpc::dynamics_kernel, dim3((unsigned)blocks), dim3(64), 0,
                      (hipStream_t)stream, pl->kp.N, (double)dt, B, mass, inertia, r_feet, xref, Ad,
                      Bd, gd);
@@ -319,7 +321,11 @@ int cmpc_generate_traj(cmpc_plan* pl, int64_t B, double dt, const float* x0, dou
   if (!x0 || !pos_des || !cmd || !t_now || !gait || !foot_lever || !hip || !xref || !contact ||
       !r_feet)
     return fail(CMPC_E_INVALID, "cmpc_generate_traj: null array argument");
-  const long long blocks = B < 8192 ? B : 8192;  // grid-stride, one wave per robot
+#ifndef CMPC_TRAJ_GRID_CAP
+#define CMPC_TRAJ_GRID_CAP 8192
+#endif
+  const long long cap = CMPC_TRAJ_GRID_CAP;
+  const long long blocks = B < cap ? B : cap;  // grid-stride, one wave per robot
   hipLaunchKernelGGL(cmpc::traj_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
                      pl->kp.N, dt, B, x0, pos_des, cmd, t_now, gait, foot_lever, hip, xref,
                      contact, r_feet);

@@ -69,6 +69,12 @@ __global__ void __launch_bounds__(64) traj_kernel(int N, double dt, int64_t B,
     // :72-73 world velocity command R_z(yaw) [vx, vy, 0]
     const double cy = cos(yaw), sy = sin(yaw);
     const double vwx = cy * vxb - sy * vyb, vwy = sy * vxb + cy * vyb;
+    // :125-130 body-frame base velocity R_world_to_body v_world, R_world_to_body = (R_z R_y R_x)'
+    // of the current state (go2_robot_data.py:211-216): rows 0, 1 of R' = columns 0, 1 of R;
+    // v_world has no z component
+    const double cr = cos(roll), sr = sin(roll), cp = cos(pitch), sp = sin(pitch);
+    const double vbx = (cy * cp) * vwx + (sy * cp) * vwy;
+    const double vby = (cy * sp * sr - sy * cr) * vwx + (sy * sp * sr + cy * cr) * vwy;
 
     // ---- x_ref (N x 12), entries e = lane + 64 j ----
     float* xr = xref + b * (int64_t)N * 12;
@@ -120,17 +126,11 @@ __global__ void __launch_bounds__(64) traj_kernel(int N, double dt, int64_t B,
           r0 = fl[0]; r1 = fl[1]; r2 = fl[2];
         } else {
           const int j = (63 - __clzll((long long)cand)) >> 2;  // last take-off step
-          // dummy model at step j (:122-132): base = pos_traj[:, j], R_z(yaw_traj[j]),
-          // body-frame base velocity R_world_to_body v_world (:125-130)
+          // dummy model at step j (:122-132): base = pos_traj[:, j], R_z(yaw_traj[j])
           const double t = (double)(j + 1) * dt;
           const double bx = pdx + vwx * t, by = pdy + vwy * t, bz = pdz + 0.0 * t;
           const double yj = yaw + wz * t;
           const double cj = cos(yj), sj = sin(yj);
-          // R_world_to_body = (R_z R_y R_x)' of the current state (go2_robot_data.py:211-216)
-          const double cr = cos(roll), sr = sin(roll), cp = cos(pitch), sp = sin(pitch);
-          // rows 0, 1 of R' = columns 0, 1 of R = R_z R_y R_x; v_world has no z component
-          const double vbx = (cy * cp) * vwx + (sy * cp) * vwy;
-          const double vby = (cy * sp * sr - sy * cr) * vwx + (sy * sp * sr + cy * cr) * vwy;
           // gait.py:40-74 touchdown prediction at take-off
           const double t_swing = (1.0 - duty) * period, t_stance = duty * period;
           const double pred = (t_swing + 0.5 * t_stance) / 2.0;

@@ -175,6 +175,17 @@ struct Cfg {
   static constexpr int WPE = CMPC_WPE_OVERRIDE;
 };
 
+// Polish sessions and their face sets.  A session starts from ADMM's face set and repairs it
+// (primal-dual active-set steps, one factorization each).  Two memories cut the factorizations
+// that hard instances used to spend on cycling:
+//  * within a session, a repair that returns to a face set the session already tried ends the
+//    session (the repair sequence has entered a cycle);
+//  * the starting sets of the last kFailMem failed sessions are remembered; ADMM's face set can
+//    stay "stable" while still wrong, and a session that starts from a remembered set polishes
+//    it once more (it may pass now, from ADMM's better iterate) but makes no repairs.
+constexpr int kFailMem = 4;
+constexpr int kTryMem = 8;
+
 template <int NC>
 struct Smem {
   alignas(16) float Bt[NC * 12];   // param-space input matrix, column p at Bt[12p .. 12p+11]
@@ -209,6 +220,8 @@ struct Smem {
   int code[kMaxTri];               // face code of triple t
   int pcode[kMaxTri];              // face code of the previous ADMM iteration
   int fpk[kMaxTri];                // polish: params of triple t, px | py << 8 | pz << 16 (255 none)
+  uint8_t fpat[kFailMem][kMaxTri]; // starting face sets of failed polish sessions
+  uint8_t tpat[kTryMem][kMaxTri];  // face sets tried in the current session (0 = its start)
 };
 
 __device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * (I + 1)) / 2 + J; }
@@ -857,6 +870,44 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 
 // ------------------------------------------------------------------------------------------
 // one QP instance on one wave
+// A polish session starts from the face set in s.code: record it as the session's first tried
+// set and look it up among the starting sets of failed sessions.  Returns the session's repair
+// budget (none for a remembered set).
+template <int NC>
+__device__ __forceinline__ int session_start(Smem<NC>& s, const KParams& P, int ntri, int nfail,
+                                             int& ntried, bool& seen) {
+  const int l = opaque_lane();
+  WSYNC();
+  uint8_t c = 0;
+  if (l < ntri) {
+    c = (uint8_t)s.code[l];
+    s.tpat[0][l] = c;
+  }
+  ntried = 1;
+  seen = false;
+#pragma unroll
+  for (int k = 0; k < kFailMem; ++k) {
+    if (k >= nfail) break;  // uniform: only this instance's failed sessions
+    const bool diff = (l < ntri) && (s.fpat[k][l] != c);
+    seen |= (__any(diff) == 0);
+  }
+  return seen ? 0 : P.polish_repairs;
+}
+
+// Has the current session already tried the repaired face set in s.tcnt?
+template <int NC>
+__device__ __forceinline__ bool tried_before(Smem<NC>& s, int ntri, int ntried) {
+  const int l = opaque_lane();
+  WSYNC();
+  const uint8_t c = (l < ntri) ? (uint8_t)s.tcnt[l] : 0;
+  bool hit = false;
+  for (int k = 0; k < ntried; ++k) {  // uniform trip count
+    const bool diff = (l < ntri) && (s.tpat[k][l] != c);
+    hit |= (__any(diff) == 0);
+  }
+  return hit;
+}
+
 // ------------------------------------------------------------------------------------------
 template <int NC>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
@@ -967,6 +1018,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   // ADMM state (x, z, y of triple t at 3t .. 3t+2) lives in LDS, not in registers
 
   int status = -2, iters = 0;
+#ifdef CMPC_DIAG_COUNTS
+  int dg_fact = 0, dg_pol = 0;
+  const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
+#endif
   bool polished = false;
   float rho = P.rho0;
   float rp = 0.f, rd = 0.f, np_ = 0.f, nd = 0.f;
@@ -978,6 +1033,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int it = 0;
   int repairs_left = 0;
   bool parked = false;    // the ADMM inverse is in the park slab
+  int nfail = 0;          // failed sessions so far (the memory holds the last kFailMem)
+  int ntried = 0;         // face sets tried in the current session
+  bool seen_start = false;  // the current session started from a remembered failed set
   const float alpha = P.alpha;
   if (n == 0) status = 1;
   if (n > 0 && in.w_init != nullptr) {
@@ -986,14 +1044,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     // repairs fail, ADMM starts from the warm (x, z, y) as above
     WSYNC();
     if (lane < ntri) s.code[lane] = s.pcode[lane];
+    repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
     nact = polish_setup<NC>(s, P, Bg, ntri);
     shift = P.sigma;
     in_polish = true;
-    repairs_left = P.polish_repairs;
   }
   while (n > 0) {
     if (refactor) {  // the only condense + invert call site
       CMPC_CNT(8, 1);
+#ifdef CMPC_DIAG_COUNTS
+      ++dg_fact;
+#endif
       CMPC_T0(t_c);
       condense_tiles<NC>(s, P, M, nact, shift);
       CMPC_ACC(0, t_c);
@@ -1029,13 +1090,24 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         status = 1;
         break;
       }
-      if (repairs_left > 0 && changed) {  // re-polish on the repaired face set
+      if (repairs_left > 0 && changed && !tried_before<NC>(s, ntri, ntried)) {
+        // re-polish on the repaired face set
         --repairs_left;
-        if (lane < ntri) s.code[lane] = s.tcnt[lane];
+        if (lane < ntri) {
+          s.code[lane] = s.tcnt[lane];
+          if (ntried < kTryMem) s.tpat[ntried][lane] = (uint8_t)s.tcnt[lane];
+        }
+        if (ntried < kTryMem) ++ntried;
         nact = polish_setup<NC>(s, P, Bg, ntri);
         shift = P.sigma;
         refactor = true;
         continue;
+      }
+      // the session failed: remember its starting face set (unless it came from the memory)
+      if (!seen_start) {
+        const int l = opaque_lane();
+        if (l < ntri) s.fpat[nfail % kFailMem][l] = s.tpat[0][l];
+        ++nfail;
       }
       // restore the basis and the parked ADMM inverse (or rebuild it first), continue ADMM
       build_admm_basis<NC>(s, P, Bg, ntri);
@@ -1132,6 +1204,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     CMPC_ACC(7, t_rest);
     if (do_pol) {
       CMPC_CNT(9, 1);
+#ifdef CMPC_DIAG_COUNTS
+      ++dg_pol;
+#endif
       CMPC_T0(t_ps);
 #ifndef CMPC_NO_PARK
       parked = !refactor;  // a pending refactor (rho changed) makes the current inverse stale
@@ -1139,12 +1214,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #else
       parked = false;      // a failed polish refactors the ADMM matrix instead
 #endif
+      repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
       nact = polish_setup<NC>(s, P, Bg, ntri);
       CMPC_ACC(14, t_ps);
       shift = P.sigma;
       refactor = true;
       in_polish = true;
-      repairs_left = P.polish_repairs;
     }
   }
   if (!polished) {
@@ -1185,8 +1260,13 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     }
   }
   if (lane == 0) {
+#ifdef CMPC_DIAG_COUNTS  // diagnostic build: iters | attempts | factorizations, cycles / 16
+    out.status[b] = (int)((__builtin_amdgcn_s_memtime() - dg_t0) >> 4);
+    out.iters[b] = iters + 1000 * dg_pol + 1000000 * dg_fact;
+#else
     out.status[b] = status;
     out.iters[b] = iters;
+#endif
   }
   CMPC_CNT(11, iters);
   CMPC_ACC(15, t_out);

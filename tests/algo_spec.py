@@ -14,7 +14,7 @@ F32 = np.float32
 class Params:
     def __init__(self, N=16, Q=None, R=None, mu=0.8, fz_min=10.0, rho=1e-4, sigma=1e-6,
                  alpha=1.6, max_iter=400, stable_checks=3, adaptive_interval=25,
-                 eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=3):
+                 eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=6):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -208,6 +208,7 @@ def solve(inst, p: Params):
 
     self_newcode = [None]
 
+    failed_starts = []
     rho = p.rho
     L = admm_matrix(rho)
     x = np.zeros(nf, F32); z = np.zeros(nf, F32); y = np.zeros(nf, F32)
@@ -233,18 +234,27 @@ def solve(inst, p: Params):
             stable = 0
         prev_code = code
         if stable >= p.stable_checks:
+            # a session: polish ADMM's face set, then repair it.  A set that started a failed
+            # session before is polished once more without repairs; a repair that returns to a
+            # set this session already tried ends the session (cmpc_wave.hip kFailMem/kTryMem).
+            start = code.tobytes()
+            seen = start in failed_starts[-4:]
+            tried = [start]
             ok, u = polish(z, code)
             rep = 0
-            while not ok and rep < p.repairs:
+            while not ok and rep < (0 if seen else p.repairs):
                 c2 = self_newcode[0]
-                if np.array_equal(c2, code):
+                if np.array_equal(c2, code) or c2.tobytes() in tried[:8]:
                     break
                 code = c2
+                tried.append(code.tobytes())
                 ok, u = polish(z, code)
                 rep += 1
             stable = -p.stable_checks  # back off before the next attempt
             if ok:
                 status = 1; U = u; break
+            if not seen:
+                failed_starts.append(start)
         if p.adaptive_interval and it % p.adaptive_interval == 0:
             rp = np.max(np.abs(x - z)); rd = np.max(np.abs(g + y))
             npn = max(np.max(np.abs(x)), np.max(np.abs(z)), 1e-30)

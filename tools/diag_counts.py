@@ -1,0 +1,46 @@
+"""Diagnostic: per-instance cost anatomy (libcmpc_diag.so, -DCMPC_DIAG_COUNTS): iterations,
+polish attempts, factorizations and wave cycles per instance; how much of the batch's wave time
+the slowest instances take."""
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
+
+
+def main():
+    import torch
+    from cmpc import _lib
+    _lib._lib = _lib.load(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_diag.so")
+    from cmpc import Plan, SolverParams, to_device_batch, synth
+    over = dict(a.split("=") for a in sys.argv[1:])
+    over = {k: type(getattr(SolverParams, k))(float(v) if "." in v else int(v)) for k, v in over.items()}
+    plan = Plan(SolverParams(max_batch=65536, **over))
+    for cfg in (1, 2):
+        b = synth.make_batch(65536, seed=cfg, mixed=cfg == 2)
+        d = to_device_batch(b)
+        w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+        torch.cuda.synchronize()
+        cyc = st.cpu().numpy().astype(np.float64) * 16
+        code = it.cpu().numpy().astype(np.int64)
+        iters, pol, fac = code % 1000, (code // 1000) % 1000, code // 1000000
+        order = np.argsort(-cyc)
+        tot = cyc.sum()
+        print(f"cfg{cfg} {over}: mean cycles {cyc.mean():.0f}  iters mean {iters.mean():.2f}  "
+              f"polish {pol.mean():.2f}  fact {fac.mean():.2f}")
+        for frac in (0.001, 0.01, 0.05):
+            k = max(1, int(frac * len(cyc)))
+            top = order[:k]
+            print(f"  top {frac*100:.1f}%: {100*cyc[top].sum()/tot:5.1f}% of cycles  iters {iters[top].mean():.1f}  "
+                  f"polish {pol[top].mean():.1f}  fact {fac[top].mean():.1f}  cycles {cyc[top].mean():.0f}")
+        print("  slowest instances:", order[:8].tolist(), "iters", iters[order[:8]].tolist(),
+              "fact", fac[order[:8]].tolist())
+        print(f"  max: cycles {cyc.max():.0f} iters {iters[order[0]]} polish {pol[order[0]]} fact {fac[order[0]]}")
+        for q in (50, 90, 99, 99.9):
+            print(f"  p{q}: cycles {np.percentile(cyc, q):.0f} iters {np.percentile(iters, q):.0f} fact {np.percentile(fac, q):.0f}")
+
+
+if __name__ == "__main__":
+    main()
