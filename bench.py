@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--tick-steps", type=int, default=5,
                     help="timed steps of the all-on-device MPC tick (generate_traj -> "
                          "build_dynamics -> solve); 0 = skip")
+    ap.add_argument("--leg-steps", type=int, default=5,
+                    help="timed steps of the on-device leg controller (cmpc_leg_torque); 0 = skip")
     ap.add_argument("--param", action="append", default=[],
                     help="SolverParams override key=value (experiments)")
     ap.add_argument("--lib", type=str, default=None,
@@ -324,6 +326,52 @@ def main():
                 "solved_frac": float((st == 1).float().mean().item()),
                 "iters_mean": float(tick_it.mean())}
 
+    # the consumer of U[:, 0] -- the 1 kHz leg controller
+    # (leg_controller.py:43-112) for every robot of the batch, on the device, with synthetic
+    # Pinocchio quantities (random SPD M) and the solver's own forces.  HBM-bound.
+    leg = None
+    if args.leg_steps > 0:
+        from cmpc import leg_state
+        gl = torch.Generator(device=dev).manual_seed(77 + rank)
+        f64 = torch.float64
+        rn = lambda *sh, s=1.0: torch.randn(sh, generator=gl, device=dev, dtype=f64) * s  # noqa: E731
+        Am = rn(B, 18, 18)
+        Ml = Am @ Am.transpose(1, 2) / 18 + 0.3 * torch.eye(18, device=dev, dtype=f64)
+        del Am
+        li = dict(J_foot=rn(B, 4, 3, 3, s=0.2), J_full=rn(B, 4, 3, 18, s=0.2), M=Ml,
+                  C=rn(B, 18, 18, s=0.1), g=rn(B, 18, s=3.0), dq=rn(B, 18), Jdot_dq=rn(B, 4, 3, s=0.3),
+                  foot_pos=rn(B, 4, 3, s=0.3), foot_vel=rn(B, 4, 3, s=0.3), body=rn(B, 16, s=0.5),
+                  hip=rn(4, 3, s=0.2))
+        tl = torch.rand(B, generator=gl, device=dev, dtype=f64) * 5
+        gait_l = torch.tensor([1 / 3.0, 0.6, 0.5, 0.0, 0.0, 0.5], device=dev, dtype=f64).repeat(B, 1)
+        stl = leg_state(B, dev)
+        taul = torch.empty((B, 12), dtype=f64, device=dev)
+
+        def leg_step():
+            plan.leg_torque(tl, gait_l, w[:, 192:], li["J_foot"], li["J_full"], li["M"], li["C"],
+                            li["g"], li["dq"], li["Jdot_dq"], li["foot_pos"], li["foot_vel"],
+                            li["body"], li["hip"], stl, out=taul, stream=stream)
+        for _ in range(2):
+            leg_step()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(args.leg_steps):
+            tl.add_(0.001)
+            leg_step()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        leg_ms = e0.elapsed_time(e1) / args.leg_steps
+        # bytes the controller reads / writes per robot (fp64; C: the 12 leg-joint rows)
+        leg_bytes = (8 + 48 + 48 + 288 + 1728 + 2592 + 1728 + 96 + 144 + 96 * 3 + 128 + 256
+                     + 96 + 256)
+        gbs_l = leg_bytes * B / (leg_ms * 1e-3) / 1e9
+        leg = {"kernel": "leg_kernel", "ms_per_step": leg_ms, "robots_per_s": B / (leg_ms * 1e-3),
+               "roofline": {"bound": "hbm", "achieved": gbs_l, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": gbs_l / HBM_PEAK_GBS, "bytes_per_robot": leg_bytes},
+               "note": "includes the small add_ on t per step; trot gait, 2 legs swing most ticks"}
+        del li, Ml
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, args.cpu_seconds)
@@ -364,6 +412,7 @@ def main():
             "dynamics": dyn,
             "warm_start": warm,
             "tick": tick,
+            "leg_controller": leg,
             "params_override": over or None,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},

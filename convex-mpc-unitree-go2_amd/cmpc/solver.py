@@ -262,6 +262,53 @@ class Plan:
         return xref, contact, r_feet
 
 
+    def leg_torque(self, t, gait, force, J_foot, J_full, M, C, g, dq, Jdot_dq, foot_pos, foot_vel,
+                   body, hip, state, tau_max=45.0, out=None, stream=None):
+        """The reference's leg controller tick for B robots (cmpc_leg_torque, include/cmpc.h;
+        leg_controller.py:43-112 + the clip of test_MPC.py:227-228).  ``force`` is (B, 12) fp32
+        or a (B, >=12) fp32 view whose rows start at U[:, 0] (e.g. w[:, 12N:]); everything else
+        fp64 device tensors; ``state`` (B, 4, 8) is updated in place (initialise with
+        :func:`leg_state`).  Returns tau (B, 12) fp64."""
+        B = t.shape[0]
+        f64 = torch.float64
+        _dev_tensor(t, "t", f64, (B,))
+        _dev_tensor(gait, "gait", f64, (B, 6))
+        if (not isinstance(force, torch.Tensor) or force.device.type != "cuda" or
+                force.dtype != torch.float32 or force.dim() != 2 or force.shape[0] != B or
+                force.shape[1] < 12 or force.stride(1) != 1):
+            raise ValueError("force must be a (B, >=12) fp32 device tensor with unit column stride")
+        for name, x, shp in (("J_foot", J_foot, (B, 4, 3, 3)), ("J_full", J_full, (B, 4, 3, 18)),
+                             ("M", M, (B, 18, 18)), ("C", C, (B, 18, 18)), ("g", g, (B, 18)),
+                             ("dq", dq, (B, 18)), ("Jdot_dq", Jdot_dq, (B, 4, 3)),
+                             ("foot_pos", foot_pos, (B, 4, 3)), ("foot_vel", foot_vel, (B, 4, 3)),
+                             ("body", body, (B, 16)), ("hip", hip, (4, 3)),
+                             ("state", state, (B, 4, 8))):
+            _dev_tensor(x, name, f64, shp)
+        tau = torch.empty((B, 12), dtype=f64, device=t.device) if out is None else out
+        _dev_tensor(tau, "tau", f64, (B, 12))
+        if stream is None:
+            stream = torch.cuda.current_stream(t.device)
+        sp = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+        with torch.cuda.device(t.device):
+            rc = self.lib.cmpc_leg_torque(
+                self._h, ctypes.c_int64(B), P(t), P(gait), P(force),
+                ctypes.c_int64(force.stride(0)), *[P(x) for x in (J_foot, J_full, M, C, g, dq,
+                                                               Jdot_dq, foot_pos, foot_vel, body,
+                                                               hip, state)],
+                ctypes.c_double(tau_max), P(tau), sp)
+        _check(self.lib, rc, "cmpc_leg_torque")
+        return tau
+
+
+def leg_state(B: int, device="cuda") -> torch.Tensor:
+    """Fresh leg-controller memory for cmpc_leg_torque: last mask 2 (LegController.__init__,
+    leg_controller.py:40-41), everything else 0."""
+    s = torch.zeros((B, 4, 8), dtype=torch.float64, device=device)
+    s[:, :, 0] = 2.0
+    return s
+
+
 def to_device_batch(batch: dict, device="cuda") -> dict:
     """float64/uint8 numpy batch (cmpc.synth layout) -> contiguous device tensors."""
     out = {}

@@ -15,6 +15,7 @@
 #include "cmpc_wave.hip"      // solve kernels: same translation unit
 #include "cmpc_dynamics.hip"  // QP-data (discrete dynamics) kernel
 #include "cmpc_traj.hip"      // reference trajectory / contact table / foot levers kernel
+#include "cmpc_leg.hip"       // leg controller (stance torque mapping, swing) kernel
 
 struct cmpc_plan {
   cmpc_params p;
@@ -331,6 +332,30 @@ int cmpc_generate_traj(cmpc_plan* pl, int64_t B, double dt, const float* x0, dou
                      contact, r_feet);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "traj_kernel launch");
+  return CMPC_OK;
+}
+
+int cmpc_leg_torque(cmpc_plan* pl, int64_t B, const double* t, const double* gait,
+                    const float* force, int64_t force_stride, const double* J_foot,
+                    const double* J_full, const double* M, const double* C, const double* g,
+                    const double* dq, const double* Jdot_dq, const double* foot_pos,
+                    const double* foot_vel, const double* body, const double* hip,
+                    double* state, double tau_max, double* tau, void* stream) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_leg_torque: null plan");
+  if (B < 0) return fail(CMPC_E_INVALID, "cmpc_leg_torque: negative batch");
+  if (force_stride < 12) return fail(CMPC_E_INVALID, "cmpc_leg_torque: force_stride must be >= 12");
+  if (!std::isfinite(tau_max)) return fail(CMPC_E_INVALID, "cmpc_leg_torque: tau_max must be finite");
+  if (B == 0) return CMPC_OK;
+  if (!t || !gait || !force || !J_foot || !J_full || !M || !C || !g || !dq || !Jdot_dq ||
+      !foot_pos || !foot_vel || !body || !hip || !state || !tau)
+    return fail(CMPC_E_INVALID, "cmpc_leg_torque: null array argument");
+  cmpc::LegArgs a{t, gait, force, force_stride, J_foot, J_full, M, C, g, dq, Jdot_dq, foot_pos,
+                  foot_vel, body, hip, state, tau_max, tau};
+  const long long blocks = B < 16384 ? B : 16384;  // grid-stride, one wave per robot
+  hipLaunchKernelGGL(cmpc::leg_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
+                     B, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "leg_kernel launch");
   return CMPC_OK;
 }
 

@@ -163,6 +163,34 @@ int cmpc_generate_traj(cmpc_plan* plan, int64_t B, double dt, const float* x0, d
                        const float* foot_lever, const float* hip, float* xref, uint8_t* contact,
                        float* r_feet, void* stream);
 
+/* The reference's 1 kHz leg controller for B robots (the consumer of the
+ * QP's first forces): LegController.compute_leg_torque for legs FL FR RL RR
+ * (leg_controller.py:43-112; test_MPC.py:199-225) -- stance tau = J_foot' (-f) (:100-101),
+ * swing tau = J_foot' (KP e_p + KD e_v + Lambda (a_des - Jdot dq)) + (C dq + g)[leg] with
+ * Lambda = (J_full M^-1 J_full')^-1 (:75-98) and the swing trajectory planned at take-off
+ * (gait.py:77-174) -- then clipped to +-tau_max (test_MPC.py:227-228; tau_max <= 0: no clip).
+ * Pinocchio's quantities are inputs (fp64, as the reference computes them):
+ *   t        [B]           time_now;  gait [B][6] as for cmpc_generate_traj
+ *   force    fp32 rows of 12, row stride force_stride (>= 12) floats: U[:, 0] of each robot,
+ *            e.g. w_out + 12 N with stride 24 N (test_MPC.py:196)
+ *   J_foot   [B][4][3][3]  compute_3x3_foot_Jacobian_world(leg) (go2_robot_data.py:286-301)
+ *   J_full   [B][4][3][18] compute_full_foot_Jacobian_world(leg) (:347-353)
+ *   M, C     [B][18][18]   compute_dynamcis_terms() (:355-360);  g, dq [B][18]
+ *   Jdot_dq, foot_pos, foot_vel [B][4][3]  compute_Jdot_dq_world, get_single_foot_state_in_world
+ *   body     [B][16]  base_pos(3), pos_com_world(3), vel_com_world(3), yaw (R_z),
+ *                     yaw_rate_des_world, x/y_pos_des_world, x/y_vel_des_world, 0
+ *                     (what gait.py:80-96 reads; the des values generate_traj stored)
+ *   hip      [4][3]   get_hip_offset(leg)
+ *   state    [B][4][8] in/out, the controller's memory: last mask (initialise to 2), take-off
+ *                     time, swing start (3), touchdown (3)  (leg_controller.py:41, 67-72, 104)
+ *   tau      [B][12]  out, fp64. */
+int cmpc_leg_torque(cmpc_plan* plan, int64_t B, const double* t, const double* gait,
+                    const float* force, int64_t force_stride, const double* J_foot,
+                    const double* J_full, const double* M, const double* C, const double* g,
+                    const double* dq, const double* Jdot_dq, const double* foot_pos,
+                    const double* foot_vel, const double* body, const double* hip,
+                    double* state, double tau_max, double* tau, void* stream);
+
 /* Measurement hooks (not on the reference's interface; used by bench.py).  While enabled,
  * cmpc_solve records a hipEvent pair around every solve-kernel launch (one per free-variable
  * bin; the bins run concurrently on plan-internal streams joined back to `stream`).  cmpc_plan_timing_read waits for the recorded events, returns the

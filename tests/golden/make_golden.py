@@ -14,7 +14,12 @@
    state (scipy ``Rotation``).  Inputs are fp32-representable (the C-ABI's boundary type) except
    time and gait, which the C-ABI takes in float64.  Pins oracle/traj_ref.py and
    ``cmpc_generate_traj``.
-3. ``qp_cfg1.npz`` / ``qp_cfg2.npz`` -- synthetic batches (cmpc.synth, SURVEY.md 8(d) configs
+3. ``leg_ticks.npz`` -- consecutive 1 kHz ticks of the reference's ``LegController.compute_leg_torque``
+   for the four legs (leg_controller.py:43-112, with ``Gait.compute_swing_traj_and_touchdown`` /
+   ``make_swing_trajectory``, gait.py:77-174) on a stand-in robot that returns given Pinocchio
+   quantities (Jacobians, M, C, g, dq, foot states: synthetic, fp32-representable; M SPD).
+   Pins oracle/leg_ref.py and ``cmpc_leg_torque``.
+4. ``qp_cfg1.npz`` / ``qp_cfg2.npz`` -- synthetic batches (cmpc.synth, SURVEY.md 8(d) configs
    1 and 2) with their KKT-certified float64 optimum from oracle/tight_solver.py, in the
    reference layout (w, lam_x, lam_a) plus the certificate residuals.
 
@@ -208,6 +213,109 @@ def make_traj_ticks(n_robots: int = 10, n_ticks: int = 6):
     print("traj_ticks.npz:", len(rec["N"]), "ticks")
 
 
+class LegGo2:
+    """Stand-in for PinGo2Model exposing what LegController / Gait's swing planning read
+    (go2_robot_data.py:171-173, 271-360): values set per tick by make_leg_ticks."""
+    LEGS = ("FL", "FR", "RL", "RR")
+
+    def __init__(self, hip):
+        self.current_config = _Cfg()
+        self._hip = {n: hip[i].copy() for i, n in enumerate(self.LEGS)}
+
+    def set(self, J_foot, J_full, M, C, g, dq, Jdd, fpos, fvel, body):
+        self._Jf, self._Jfull, self._M, self._C, self._g = J_foot, J_full, M, C, g
+        self._dq, self._Jdd, self._fp, self._fv = dq, Jdd, fpos, fvel
+        self.current_config.base_pos = body[0:3].copy()
+        self.current_config.get_dq = lambda: self._dq.copy()
+        self.pos_com_world, self.vel_com_world = body[3:6].copy(), body[6:9].copy()
+        c, s_ = np.cos(body[9]), np.sin(body[9])
+        self.R_z = np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1.0]])
+        self.yaw_rate_des_world = body[10]
+        self.x_pos_des_world, self.y_pos_des_world = body[11], body[12]
+        self.x_vel_des_world, self.y_vel_des_world = body[13], body[14]
+
+    def _i(self, leg):
+        return self.LEGS.index(leg)
+
+    def get_hip_offset(self, leg):
+        return self._hip[leg]
+
+    def compute_3x3_foot_Jacobian_world(self, leg):
+        return self._Jf[self._i(leg)].copy()
+
+    def compute_full_foot_Jacobian_world(self, leg):
+        return self._Jfull[self._i(leg)].copy()
+
+    def compute_dynamcis_terms(self):
+        return self._g.copy(), self._C.copy(), self._M.copy()
+
+    def get_single_foot_state_in_world(self, leg):
+        return self._fp[self._i(leg)].copy(), self._fv[self._i(leg)].copy()
+
+    def compute_Jdot_dq_world(self, leg):
+        return self._Jdd[self._i(leg)].copy()
+
+
+def make_leg_ticks(n_robots: int = 5, n_ticks: int = 150):
+    """Consecutive 1 kHz ticks of the reference's leg controller, per robot (see module doc)."""
+    gait_mod, _ = import_reference()
+    import leg_controller as lc_mod
+    rng = np.random.default_rng(13)
+    f32 = lambda a: np.asarray(np.float32(a), dtype=np.float64)  # noqa: E731
+    hip = f32(np.array([[0.1934, 0.142, 0.0], [0.1934, -0.142, 0.0],
+                        [-0.1934, 0.142, 0.0], [-0.1934, -0.142, 0.0]]))
+    fixed = {k: [] for k in ("J_foot", "J_full", "M", "C")}
+    rec = {k: [] for k in ("robot", "t", "gait", "force", "g", "dq", "Jdot_dq", "foot_pos",
+                           "foot_vel", "body", "tau")}
+    for r in range(n_robots):
+        hz = [5.0, 4.0, 6.0, 5.0, 4.5][r % 5]
+        duty = [0.5, 0.6, 0.45, 0.55, 0.5][r % 5]
+        offs = np.array([0.5, 0.0, 0.0, 0.5]) if r % 2 == 0 else rng.uniform(0, 1, 4)
+        g_ = gait_mod.Gait(hz, duty)
+        J_foot = f32(rng.normal(0, 0.2, (4, 3, 3)))
+        J_full = f32(rng.normal(0, 0.2, (4, 3, 18)))
+        J_full[:, :, 6:] = 0.0
+        for l in range(4):
+            J_full[l, :, 6 + 3 * l:9 + 3 * l] = J_foot[l]
+        Araw = rng.normal(0, 1, (18, 18))
+        M = f32(Araw @ Araw.T / 18 + np.diag(rng.uniform(0.05, 1.0, 18)))
+        C = f32(rng.normal(0, 0.1, (18, 18)))
+        for k, v in (("J_foot", J_foot), ("J_full", J_full), ("M", M), ("C", C)):
+            fixed[k].append(v)
+        go2 = LegGo2(hip)
+        ctrl = lc_mod.LegController()
+        t = float(rng.uniform(0, 1.0))
+        gait_mod.PHASE_OFFSET = offs.copy()
+        yaw = float(rng.uniform(-np.pi, np.pi))
+        for _ in range(n_ticks):
+            body = f32(np.concatenate([rng.normal(0, 0.5, 2), [0.27 + 0.01 * rng.normal()],
+                                       rng.normal(0, 0.5, 2), [0.27 + 0.01 * rng.normal()],
+                                       rng.normal(0, 0.3, 3), [yaw], [rng.uniform(-2, 2)],
+                                       rng.normal(0, 0.5, 2), rng.uniform(-0.8, 0.8, 2), [0.0]]))
+            gv, dq = f32(rng.normal(0, 3, 18)), f32(rng.normal(0, 1, 18))
+            Jdd, fpos, fvel = (f32(rng.normal(0, 0.3, (4, 3))) for _ in range(3))
+            force = f32(rng.normal(0, 40, 12))
+            go2.set(J_foot, J_full, M, C, gv, dq, Jdd, fpos, fvel, body)
+            tau = np.zeros(12)
+            for l, leg in enumerate(LegGo2.LEGS):
+                out = ctrl.compute_leg_torque(leg, go2, g_, force[3 * l:3 * l + 3], t)
+                tau[3 * l:3 * l + 3] = out.tau
+            for k, v in (("robot", r), ("t", t), ("gait", [g_.gait_period, duty, *offs]),
+                         ("force", force), ("g", gv), ("dq", dq), ("Jdot_dq", Jdd),
+                         ("foot_pos", fpos), ("foot_vel", fvel), ("body", body), ("tau", tau)):
+                rec[k].append(np.array(v, copy=True))
+            t += 0.001
+            yaw += 0.002
+    gait_mod.PHASE_OFFSET = np.array([0.5, 0.0, 0.0, 0.5])
+    out = {k: np.stack(v) for k, v in rec.items()}
+    for k in ("force", "g", "dq", "Jdot_dq", "foot_pos", "foot_vel", "body"):
+        out[k] = out[k].astype(np.float32)       # fp32-representable inputs, stored compactly
+    out.update({k: np.stack(v).astype(np.float32) for k, v in fixed.items()})
+    out["hip"] = hip.astype(np.float32)
+    np.savez_compressed(HERE / "leg_ticks.npz", **out)
+    print("leg_ticks.npz:", len(rec["t"]), "ticks")
+
+
 def make_qp_fixture(cfg: int, B: int, name: str):
     b = synth.make_config(cfg, B=B)
     W, LX, LA, KKT = [], [], [], []
@@ -229,5 +337,6 @@ def make_qp_fixture(cfg: int, B: int, name: str):
 if __name__ == "__main__":
     make_ref_inputs()
     make_traj_ticks()
+    make_leg_ticks()
     make_qp_fixture(1, 32, "qp_cfg1.npz")
     make_qp_fixture(2, 64, "qp_cfg2.npz")

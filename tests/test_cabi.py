@@ -67,6 +67,8 @@ def test_null_arguments(lib):
     assert "cmpc_solve_warm" in lib.cmpc_last_error().decode()
     assert lib.cmpc_generate_traj(None, 1, 0.02, *([None] * 11)) == -22
     assert "cmpc_generate_traj" in lib.cmpc_last_error().decode()
+    assert lib.cmpc_leg_torque(None, 1, None, None, None, 12, *([None] * 12), 45.0, None, None) == -22
+    assert "cmpc_leg_torque" in lib.cmpc_last_error().decode()
     lib.cmpc_plan_destroy(None)
 
 
