@@ -78,6 +78,8 @@ def parse():
                          "build_dynamics -> solve); 0 = skip")
     ap.add_argument("--leg-steps", type=int, default=5,
                     help="timed steps of the on-device leg controller (cmpc_leg_torque); 0 = skip")
+    ap.add_argument("--loop-steps", type=int, default=24,
+                    help="timed closed-loop MPC ticks (config 4 shape, SRB plant); 0 = skip")
     ap.add_argument("--param", action="append", default=[],
                     help="SolverParams override key=value (experiments)")
     ap.add_argument("--lib", type=str, default=None,
@@ -372,6 +374,43 @@ def main():
                "note": "includes the small add_ on t per step; trot gait, 2 legs swing most ticks"}
         del li, Ml
 
+    # BASELINE config 4 shape: robots in closed loop, every MPC tick on the device
+    # (generate_traj -> build_dynamics -> warm solve -> SRB plant for 20 leg ticks), recorded once
+    # as a HIP graph and replayed.  MuJoCo is absent: the plant is cmpc_srb_step's stand-in.
+    loop = None
+    if args.loop_steps > 0:
+        from cmpc.closed_loop import ClosedLoop
+        loop = {"plant": "cmpc_srb_step single-rigid-body stand-in (MuJoCo absent)",
+                "mpc_dt_s": 1 / 48}
+        for nb in (1024, B):
+            cl = ClosedLoop(nb, plan=plan, seed=rank)
+            rg = np.random.default_rng(100 + rank)
+            cl.set_command(np.stack([rg.uniform(-0.5, 0.5, nb), rg.uniform(-0.2, 0.2, nb),
+                                     np.full(nb, 0.27), rg.uniform(-1, 1, nb)], 1))
+            for _ in range(4):
+                cl.tick()
+            torch.cuda.synchronize(dev)
+            te = time.perf_counter()
+            for _ in range(args.loop_steps):
+                cl.tick()
+            torch.cuda.synchronize(dev)
+            eager = nb * args.loop_steps / (time.perf_counter() - te)
+            cl.capture()
+            cl.tick()
+            torch.cuda.synchronize(dev)
+            tg = time.perf_counter()
+            for _ in range(args.loop_steps):
+                cl.tick()
+            torch.cuda.synchronize(dev)
+            el = time.perf_counter() - tg
+            loop[f"robots_{nb}"] = {"robot_ticks_per_s_graph": nb * args.loop_steps / el,
+                                    "ms_per_tick_graph": el / args.loop_steps * 1e3,
+                                    "robot_ticks_per_s_eager": eager,
+                                    "solved_frac": float((cl.status == 1).float().mean().item()),
+                                    "iters_mean": float(cl.iters.float().mean().item()),
+                                    "com_z_min": float(cl.x[:, 2].min().item())}
+            del cl
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, args.cpu_seconds)
@@ -413,6 +452,7 @@ def main():
             "warm_start": warm,
             "tick": tick,
             "leg_controller": leg,
+            "closed_loop": loop,
             "params_override": over or None,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},

@@ -39,7 +39,7 @@ class CParams(ctypes.Structure):
 
 
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
-           "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_generate_traj", "cmpc_leg_torque",
+           "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_last_error", "cmpc_version")
 NUM_BINS = 4
 BIN_CAPS = (96, 128, 160, 192)
@@ -76,6 +76,10 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
         lib.cmpc_leg_torque.argtypes = ([vp, ctypes.c_int64, vp, vp, vp, ctypes.c_int64] +
                                         [vp] * 12 + [ctypes.c_double, vp, vp])
         lib.cmpc_leg_torque.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_srb_step"):
+        lib.cmpc_srb_step.argtypes = ([vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double] + [vp] * 5 +
+                                      [ctypes.c_int64] + [vp] * 5)
+        lib.cmpc_srb_step.restype = ctypes.c_int
     lib.cmpc_plan_destroy.argtypes = [vp]
     lib.cmpc_plan_destroy.restype = None
     lib.cmpc_plan_set_timing.argtypes = [vp, ctypes.c_int]

@@ -16,6 +16,7 @@
 #include "cmpc_dynamics.hip"  // QP-data (discrete dynamics) kernel
 #include "cmpc_traj.hip"      // reference trajectory / contact table / foot levers kernel
 #include "cmpc_leg.hip"       // leg controller (stance torque mapping, swing) kernel
+#include "cmpc_sim.hip"       // single-rigid-body plant (closed-loop stand-in for MuJoCo)
 
 struct cmpc_plan {
   cmpc_params p;
@@ -356,6 +357,26 @@ int cmpc_leg_torque(cmpc_plan* pl, int64_t B, const double* t, const double* gai
                      B, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "leg_kernel launch");
+  return CMPC_OK;
+}
+
+int cmpc_srb_step(cmpc_plan* pl, int64_t B, int nsub, double dt, const double* t_now,
+                  const double* gait, const float* mass, const float* inertia_body,
+                  const float* force, int64_t force_stride, const float* hip, float* x,
+                  float* feet, uint8_t* contact_state, void* stream) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_srb_step: null plan");
+  if (B < 0 || nsub < 0) return fail(CMPC_E_INVALID, "cmpc_srb_step: negative batch or nsub");
+  if (!(dt > 0.0) || !std::isfinite(dt)) return fail(CMPC_E_INVALID, "cmpc_srb_step: dt must be > 0");
+  if (force_stride < 12) return fail(CMPC_E_INVALID, "cmpc_srb_step: force_stride must be >= 12");
+  if (B == 0 || nsub == 0) return CMPC_OK;
+  if (!t_now || !gait || !mass || !inertia_body || !force || !hip || !x || !feet || !contact_state)
+    return fail(CMPC_E_INVALID, "cmpc_srb_step: null array argument");
+  const unsigned blocks = (unsigned)((B + 255) / 256);
+  hipLaunchKernelGGL(cmpc::srb_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, B, nsub,
+                     dt, t_now, gait, mass, inertia_body, force, force_stride, hip, x, feet,
+                     contact_state);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "srb_kernel launch");
   return CMPC_OK;
 }
 

@@ -191,6 +191,19 @@ int cmpc_leg_torque(cmpc_plan* plan, int64_t B, const double* t, const double* g
                     const double* foot_vel, const double* body, const double* hip,
                     double* state, double tau_max, double* tau, void* stream);
 
+/* Closed-loop stand-in for the simulator (MuJoCo is absent from this image):
+ * advance B single-rigid-body robots by nsub substeps of dt under the held ground forces U[:, 0]
+ * (rows of 12 fp32, row stride force_stride), with the gait deciding contact at each substep.
+ *   t_now [B] fp64 (start time, not advanced), gait [B][6] as above, mass [B],
+ *   inertia_body [B][3][3] (body-frame I_com), hip [4][3];
+ *   x [B][12] in/out (p, rpy, v, w_world: the MPC state), feet [B][4][3] in/out (world foot
+ *   positions, used while in stance), contact_state [B] in/out (bit l: leg l in stance).
+ * Not a reference interface: it exists to exercise the on-device tick in closed loop. */
+int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double* t_now,
+                  const double* gait, const float* mass, const float* inertia_body,
+                  const float* force, int64_t force_stride, const float* hip, float* x,
+                  float* feet, uint8_t* contact_state, void* stream);
+
 /* Measurement hooks (not on the reference's interface; used by bench.py).  While enabled,
  * cmpc_solve records a hipEvent pair around every solve-kernel launch (one per free-variable
  * bin; the bins run concurrently on plan-internal streams joined back to `stream`).  cmpc_plan_timing_read waits for the recorded events, returns the

@@ -69,6 +69,8 @@ def test_null_arguments(lib):
     assert "cmpc_generate_traj" in lib.cmpc_last_error().decode()
     assert lib.cmpc_leg_torque(None, 1, None, None, None, 12, *([None] * 12), 45.0, None, None) == -22
     assert "cmpc_leg_torque" in lib.cmpc_last_error().decode()
+    assert lib.cmpc_srb_step(None, 1, 20, 0.001, *([None] * 5), 12, *([None] * 5)) == -22
+    assert "cmpc_srb_step" in lib.cmpc_last_error().decode()
     lib.cmpc_plan_destroy(None)
 
 
