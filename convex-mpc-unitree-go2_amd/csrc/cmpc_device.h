@@ -19,6 +19,7 @@ struct KParams {
   int polish_stable;
   int polish_refine;
   int polish_repairs;
+  int latency_mode;  // set per launch: at most one wave per SIMD (small batch), see condense_tiles
 };
 
 // Device pointers of one cmpc_solve call (layouts: include/cmpc.h).

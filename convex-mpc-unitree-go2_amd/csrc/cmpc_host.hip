@@ -22,6 +22,7 @@ struct cmpc_plan {
   cmpc_params p;
   cmpc::KParams kp;
   int device;
+  int cus = 0;      // compute units of the device
   int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
   float* d_work;    // per-wave park slabs; bin q's region starts at work_off[q] (bins run concurrently)
@@ -160,6 +161,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipGetDevice"); }
   int cus = 0;
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pl->device);
+  pl->cus = cus;
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
   size_t work_floats = 0;
   for (int q = 0; q < cmpc::kNumBins; ++q) {
@@ -270,7 +272,10 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
       }
       if ((e = hipEventRecord(rec.a, bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     }
-    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(pl->threads[q]), 0, bs, pl->kp, in,
+    cmpc::KParams kp = pl->kp;
+    // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
+    kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
+    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(pl->threads[q]), 0, bs, kp, in,
                        out, pl->d_lists + (size_t)q * pl->p.max_batch, pl->d_counters + q,
                        pl->d_counters + cmpc::kNumBins + q, pl->d_work + pl->work_off[q]);
     e = hipGetLastError();

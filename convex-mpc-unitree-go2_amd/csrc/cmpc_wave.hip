@@ -238,8 +238,8 @@ __device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * 
 // whose accumulator IS the matrix tile.  Tile row I starts to receive terms at the step of its
 // first parameter; nothing of G ever goes through memory.
 template <int NC>
-__device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
-                                               f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
+__device__ __forceinline__ void condense_tiles_fwd(Smem<NC>& s, const KParams& P,
+                                                   f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
   using C = Cfg<NC>;
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
@@ -446,6 +446,156 @@ __device__ __forceinline__ void sweep_block(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL], 
     }
     sweep_block<NC, K + 1>(s, M, ng, TA, g, c, a, b);
   }
+}
+
+// Block-row condensation: the lower blocks of the same H are
+//   H[rows of step i, cols of step j <= i] = C_i' A^{i-j} B_j,   C_i = P_i B_i,
+//   P_i = sum_{t >= i} (A^{t-i})' Q2 A^{t-i} = Q2 + A' P_{i+1} A,
+// so step i only adds its own 1-2 tile rows (C_i' G_i, G_i = [A^{i-j} B_j]_{j <= i} as above)
+// instead of every active tile: ~25 % fewer MFMAs at n = 120.  A backward pass builds P_i in one
+// accumulator tile (A' P A: eight MFMAs; P is symmetric, so its accumulator layout is also its
+// A-operand layout) and stores C_i, param-major, in the G slab.  Diagonal tiles then receive
+// only the entries whose column step <= row step; the others are mirrored across.
+template <int NC>
+__device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
+                                                  f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
+  using C = Cfg<NC>;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int N = P.N;
+  n = uniform(n);
+#pragma unroll
+  for (int t = 0; t < C::NTL; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
+  float aA[4], aT[4], q2[4];  // A[c][4g + q] (A operand of A X), A[4g + q][c] (of A' X), Q2
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * g + q;
+    aA[q] = (c < 12 && r < 12) ? s.A[c * 12 + r] : 0.f;
+    aT[q] = (c < 12 && r < 12) ? s.A[r * 12 + c] : 0.f;
+    q2[q] = (r < 12 && r == c) ? s.Q2[r] : 0.f;
+  }
+  float* Cs = s.G;  // C_i columns, param-major [p][12] (the G slab is free while condensing)
+  // ---- backward: P_i and C_i = P_i B_i for i = N-1 .. 0 ----
+  f4 Pt = {q2[0], q2[1], q2[2], q2[3]};  // P_{N-1} = Q2 (diagonal)
+  WSYNC();
+  for (int i = N - 1; i >= 0; --i) {
+    const int p0 = s.off[i], p1 = s.off[i + 1];
+#pragma unroll
+    for (int J = 0; J < C::TT; ++J) {
+      if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform: chunks holding step i's params
+      const int p = 16 * J + c;
+      f4 bt = {0.f, 0.f, 0.f, 0.f};
+      if (g < 3 && p < n) bt = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+      f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d = mfma4(Pt[q], bt[q], d);  // C = P B (P symmetric)
+      if (g < 3 && p >= p0 && p < p1) *reinterpret_cast<f4*>(&Cs[p * 12 + 4 * g]) = d;
+    }
+    if (i > 0) {  // P_{i-1} = Q2 + A' P_i A
+      f4 y = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y = mfma4(Pt[q], aT[q], y);   // Y = P A
+#pragma unroll
+      for (int q = 0; q < 4; ++q) z = mfma4(aT[q], y[q], z);    // Z = A' Y
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Pt[q] = z[q] + q2[q];
+    }
+  }
+  WSYNC();
+  // ---- forward: G_t = A G_{t-1} + new columns; rows of step t += C_t' G_t ----
+  int kI[C::TT];
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) kI[I] = (16 * I < n) ? s.par[16 * I] : N;
+  f4 Gd[C::TT];
+#pragma unroll
+  for (int J = 0; J < C::TT; ++J) Gd[J] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < N; ++t) {
+    if (t > 0) {
+#pragma unroll
+      for (int J = 0; J < C::TT; ++J) {
+        if (kI[J] >= t) continue;  // uniform
+        f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d = mfma4(aA[q], Gd[J][q], d);
+        Gd[J] = d;
+      }
+    }
+    const int p0 = s.off[t], p1 = s.off[t + 1];
+#pragma unroll
+    for (int J = 0; J < C::TT; ++J) {
+      if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
+      const int p = 16 * J + c;
+      if (p >= p0 && p < p1 && g < 3) Gd[J] = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+    }
+#pragma unroll
+    for (int I = 0; I < C::TT; ++I) {
+      if (16 * I + 15 < p0 || 16 * I >= p1) continue;  // uniform: tile rows holding step t
+      const int p = 16 * I + c;
+      f4 a = {0.f, 0.f, 0.f, 0.f};
+      if (p >= p0 && p < p1 && g < 3) a = *reinterpret_cast<const f4*>(&Cs[p * 12 + 4 * g]);
+#pragma unroll
+      for (int J = 0; J <= I; ++J) {
+        f4 acc = M[tile_index(I, J)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = mfma4(a[q], Gd[J][q], acc);
+        M[tile_index(I, J)] = acc;
+      }
+    }
+  }
+  // ---- diagonal tiles: entry (r, c) with step(c) > step(r) is the mirror of (c, r) ----
+  WSYNC();
+  float* T = s.G;  // 16 x 16 scratch per tile
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    if (16 * I >= n) continue;  // uniform
+    f4 v = M[tile_index(I, I)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[(4 * g + q) * 16 + c] = v[q];
+    WSYNC();
+    const int pc = 16 * I + c;
+    const int kc = (pc < n) ? s.par[pc] : N;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pr = 16 * I + 4 * g + q;
+      const int kr = (pr < n) ? s.par[pr] : N;
+      if (kc > kr) v[q] = T[c * 16 + 4 * g + q];
+    }
+    M[tile_index(I, I)] = v;
+    WSYNC();
+  }
+  // + diag(Rt) + shift, identity on padding
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      f4 v = M[tile_index(I, J)];
+      const int col = 16 * J + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
+        else if (row == col) v[q] += s.Rt[row] + shift;
+      }
+      M[tile_index(I, J)] = v;
+    }
+  }
+  WSYNC();
+}
+
+// Which condensation: the block-row form has ~25 % fewer MFMAs but longer dependency chains.
+// With one wave per SIMD (small batches, latency) the chains are what a wave waits on either way
+// and the fewer MFMAs win (B = 256: 0.61 -> 0.48 ms); with two busy waves per SIMD the
+// forward form keeps the matrix pipe ~80 % busy and is ~5 % faster (tools/phase_bench.hip).
+template <int NC>
+__device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
+                                               f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
+  if constexpr (NC <= 128) {  // the 1-wave-per-SIMD bins would spill the second form
+    if (P.latency_mode) {      // uniform
+      condense_tiles_bc<NC>(s, P, M, n, shift);
+      return;
+    }
+  }
+  condense_tiles_fwd<NC>(s, P, M, n, shift);
 }
 
 // ------------------------------------------------------------------------------------------
