@@ -320,7 +320,7 @@ def main():
         td["pos_des"].copy_(pd0)
         tick_it = it.cpu().numpy()
         gbs_t = tr_bytes * B / (tr_ms * 1e-3) / 1e9
-        tick = {"kernel": "traj_kernel", "ms_per_step": tr_ms,
+        tick = {"kernel": "traj_group_kernel", "ms_per_step": tr_ms,
                 "roofline": {"bound": "hbm", "achieved": gbs_t, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": gbs_t / HBM_PEAK_GBS, "bytes_per_robot": tr_bytes},
                 "full_tick_per_s": tick_rate,

@@ -332,12 +332,14 @@ int cmpc_generate_traj(cmpc_plan* pl, int64_t B, double dt, const float* x0, dou
 #define CMPC_TRAJ_GRID_CAP 8192
 #endif
   const long long cap = CMPC_TRAJ_GRID_CAP;
-  const long long blocks = B < cap ? B : cap;  // grid-stride, one wave per robot
-  hipLaunchKernelGGL(cmpc::traj_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream,
-                     pl->kp.N, dt, B, x0, pos_des, cmd, t_now, gait, foot_lever, hip, xref,
-                     contact, r_feet);
+  // one wave per group of cmpc::kTrajGroup robots (grid-stride over groups)
+  const long long groups = (B + cmpc::kTrajGroup - 1) / cmpc::kTrajGroup;
+  const long long blocks = groups < cap ? groups : cap;
+  hipLaunchKernelGGL(cmpc::traj_group_kernel, dim3((unsigned)blocks), dim3(64), 0,
+                     (hipStream_t)stream, pl->kp.N, dt, B, x0, pos_des, cmd, t_now, gait,
+                     foot_lever, hip, xref, contact, r_feet);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(e, "traj_kernel launch");
+  if (e != hipSuccess) return hip_fail(e, "traj_group_kernel launch");
   return CMPC_OK;
 }
 
