@@ -135,6 +135,14 @@ __global__ void __launch_bounds__(64, 4) leg_kernel(int64_t B, LegArgs a) {
       // lower entry (i, k) = kTri[e].  Step j reads column j (unscaled) and writes it scaled,
       // A[i][k] -= A[i][j] A[k][j] / A[j][j] for k > j; one wave, so LDS reads issued before the
       // writes see the old values and the next step sees the new ones (wave-ordered LDS).
+      int ti[3], tk[3];  // this lane's lower entries (loop-invariant; -1: none)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int e = lane + 64 * q;
+        const bool ok = e < kNv * (kNv + 1) / 2;
+        ti[q] = ok ? kTriI[ok ? e : 0] : -1;
+        tk[q] = ok ? kTriK[ok ? e : 0] : -1;
+      }
       for (int j = 0; j < kNv; ++j) {
         const double ajj = Ms[j * kNv + j];
         const double rs = 1.0 / sqrt(ajj), ri = rs * rs;
@@ -143,10 +151,9 @@ __global__ void __launch_bounds__(64, 4) leg_kernel(int64_t B, LegArgs a) {
         int at[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-          const int e = lane + 64 * q;
           at[q] = -1;
-          if (e < kNv * (kNv + 1) / 2) {
-            const int i = kTriI[e], k = kTriK[e];
+          if (ti[q] >= 0) {
+            const int i = ti[q], k = tk[q];
             if (k == j && i >= j) {
               nv[q] = (i == j) ? ajj * rs : Ms[i * kNv + j] * rs;
               at[q] = i * kNv + j;
