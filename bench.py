@@ -80,6 +80,8 @@ def parse():
                     help="timed steps of the on-device leg controller (cmpc_leg_torque); 0 = skip")
     ap.add_argument("--loop-steps", type=int, default=24,
                     help="timed closed-loop MPC ticks (config 4 shape, SRB plant); 0 = skip")
+    ap.add_argument("--api-ticks", type=int, default=20,
+                    help="config 0: ticks of one robot through the CentroidalMPC drop-in; 0 = skip")
     ap.add_argument("--param", action="append", default=[],
                     help="SolverParams override key=value (experiments)")
     ap.add_argument("--lib", type=str, default=None,
@@ -411,6 +413,36 @@ def main():
                                     "com_z_min": float(cl.x[:, 2].min().item())}
             del cl
 
+    # BASELINE config 0: one robot through the reference's own API (CentroidalMPC.solve_QP, the
+    # drop-in of centroidal_mpc.py), warm-started every tick as the reference does; the reference
+    # budget per MPC tick is MPC_DT = 20.8 ms (test_MPC.py:67-68).
+    api = None
+    if args.api_ticks > 0 and rank == 0:
+        import types
+        sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
+        from centroidal_mpc import CentroidalMPC
+        one = synth.make_batch(1, seed=0)
+        traj = types.SimpleNamespace(
+            N=16, Ad=one["Ad"][0], Bd=one["Bd"][0], gd=one["gd"][0].reshape(12, 1),
+            initial_x_vec=one["x0"][0].reshape(12, 1), contact_table=one["contact"][0].astype(np.int32),
+            compute_x_ref_vec=lambda: one["xref"][0].T.copy())
+        import contextlib
+        with contextlib.redirect_stdout(sys.stderr):  # the reference's init print (:225-230)
+            mpc = CentroidalMPC(None, traj)
+        st_ms, up_ms, wall = [], [], []
+        for k in range(args.api_ticks + 2):
+            ta = time.perf_counter()
+            sol = mpc.solve_QP(None, traj, False)
+            _ = sol["x"].full()
+            if k >= 2:
+                wall.append((time.perf_counter() - ta) * 1e3)
+                st_ms.append(mpc.solve_time)
+                up_ms.append(mpc.update_time)
+        api = {"path": "CentroidalMPC(go2, traj).solve_QP -> sol['x'].full(), 1 robot, warm",
+               "solve_time_ms": float(np.median(st_ms)), "update_time_ms": float(np.median(up_ms)),
+               "wall_ms_per_tick": float(np.median(wall)), "mpc_dt_budget_ms": 1e3 / 48,
+               "return_status": mpc.solver.stats()["return_status"]}
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, args.cpu_seconds)
@@ -453,6 +485,7 @@ def main():
             "tick": tick,
             "leg_controller": leg,
             "closed_loop": loop,
+            "config0_api": api,
             "params_override": over or None,
             "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
                                 for i, c in enumerate((96, 128, 160, 192))},

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 VAR=$1
-EX="--cpu-seconds 0 --steps 20 --warm-steps 0 --dynamics-steps 0 --tick-steps 0 --leg-steps 0 --loop-steps 0"
+EX="--cpu-seconds 0 --steps 20 --warm-steps 0 --dynamics-steps 0 --tick-steps 0 --leg-steps 0 --loop-steps 0 --api-ticks 0"
 for cfg in 1 2; do
   : > gpurun_out/ab3_$cfg.txt
   for rep in 1 2 3 4; do
