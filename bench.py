@@ -82,6 +82,8 @@ def parse():
                     help="timed closed-loop MPC ticks (config 4 shape, SRB plant); 0 = skip")
     ap.add_argument("--api-ticks", type=int, default=20,
                     help="config 0: ticks of one robot through the CentroidalMPC drop-in; 0 = skip")
+    ap.add_argument("--seed-offset", type=int, default=0,
+                    help="added to the workload seed (experiments: average over batches)")
     ap.add_argument("--param", action="append", default=[],
                     help="SolverParams override key=value (experiments)")
     ap.add_argument("--lib", type=str, default=None,
@@ -119,7 +121,7 @@ def main():
     if cfg == 3:
         batch = synth.make_config(3, B=B)
     else:
-        batch = synth.make_batch(B, seed=synth.CONFIGS[cfg]["seed"] + 1000 * rank,
+        batch = synth.make_batch(B, seed=synth.CONFIGS[cfg]["seed"] + 1000 * rank + args.seed_offset,
                                  mixed=synth.CONFIGS[cfg]["mixed"])
     bins = bins_of(batch["contact"])
     d = to_device_batch(batch, dev)

@@ -1,0 +1,28 @@
+"""Diagnostic: instances of a cfg2 batch (seed offset argv[1]) that reach max_iter, with their
+iteration / polish-session / factorization counts (product and diag builds)."""
+import sys
+from pathlib import Path
+import numpy as np
+REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
+
+
+def main():
+    import torch
+    from cmpc import Plan, SolverParams, to_device_batch, synth, _lib
+    seed = 2 + int(sys.argv[1])
+    b = synth.make_batch(65536, seed=seed, mixed=True)
+    d = to_device_batch(b)
+    plan = Plan(SolverParams(max_batch=65536))
+    w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
+    torch.cuda.synchronize()
+    st, it = st.cpu().numpy(), it.cpu().numpy()
+    bad = np.nonzero(st != 1)[0]
+    print("seed", seed, "not status 1:", bad.tolist(), st[bad].tolist(), it[bad].tolist())
+    top = np.argsort(-it)[:6]
+    print("most iterations:", top.tolist(), it[top].tolist())
+    np.save(REPO / "gpurun_out/stuck_idx.npy", np.concatenate([bad, top]))
+
+
+if __name__ == "__main__":
+    main()
