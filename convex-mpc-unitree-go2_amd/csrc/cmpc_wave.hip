@@ -188,6 +188,11 @@ struct Cfg {
 //  * the starting sets of the last kFailMem failed sessions are remembered; ADMM's face set can
 //    stay "stable" while still wrong, and a session that starts from a remembered set polishes
 //    it once more (it may pass now, from ADMM's better iterate) but makes no repairs.
+#ifndef CMPC_REFINE_N  // diagnostic override of the refinement count
+#define CMPC_REFINE_N P.polish_refine
+#endif
+constexpr int kRefineExtra = 4;      // polish refinements beyond polish_refine ...
+constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least this much
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
@@ -1394,16 +1399,28 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     }
     if (in_polish) {
       CMPC_T0(t_pol);
-      float step = 3.0e38f;
-      for (int q = 0; q < P.polish_refine; ++q) {
+      // iterative refinement v -= M (grad): polish_refine steps, then more (up to
+      // kRefineExtra) while the step still contracts and is above the acceptance tolerance --
+      // an ill-conditioned face set (internal foot forces weigh only R) contracts slowly
+      float step = 3.0e38f, prev = 3.0e38f;
+      for (int q = 0; q < CMPC_REFINE_N + kRefineExtra; ++q) {
         gradient<NC>(s, P, nact, s.v, s.g);
         symv<NC>(s, M, nact, s.g, s.dl);
-        float m = 0.f;
+        float m = 0.f, mv = 1.f;
         for (int p = lane; p < nact; p += 64) {
-          s.v[p] -= s.dl[p];
+          const float vn = s.v[p] - s.dl[p];
+          s.v[p] = vn;
           m = fmaxf(m, fabsf(s.dl[p]));
+          mv = fmaxf(mv, fabsf(vn));
         }
         step = wave_max(m);
+#ifdef CMPC_TRACE
+        if (b == CMPC_TRACE && lane == 0) printf("    refine %d step %g\n", q, step);
+#endif
+        if (q + 1 >= CMPC_REFINE_N &&
+            (step <= P.polish_tol * wave_max(mv) || step > kRefineRate * prev))
+          break;
+        prev = step;
       }
       gradient<NC>(s, P, nact, s.v, s.g);  // E, L at the final point
       bool changed = false, loose = false;

@@ -165,13 +165,17 @@ def solve(inst, p: Params):
             return out
 
         v = np.array([zf[12 * k + 3 * l + {'x': 0, 'y': 1, 'z': 2}[ax]] for (k, l, ax, sx, sy) in params], F32)
-        step = np.inf
-        for _ in range(p.polish_refine):
+        step = np.inf; prev = np.inf
+        for q in range(p.polish_refine + 4):   # cmpc_wave.hip kRefineExtra, kRefineRate
             u = expand(v)
             g, _ = gradient(A, B, d, p.Q, p.R, u.reshape(N, 12))
             dv = solve_L(L, reduce(g.reshape(-1)))
             v = v - dv
             step = np.max(np.abs(dv), initial=0)
+            if q + 1 >= p.polish_refine and (step <= p.tol_polish * max(1.0, np.max(np.abs(v), initial=0))
+                                             or step > 0.5 * prev):
+                break
+            prev = step
         u = expand(v)
         g, _ = gradient(A, B, d, p.Q, p.R, u.reshape(N, 12))
         g = g.reshape(-1)
