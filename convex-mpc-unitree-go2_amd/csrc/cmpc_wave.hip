@@ -193,6 +193,7 @@ struct Cfg {
 #endif
 constexpr int kRefineExtra = 4;      // polish refinements beyond polish_refine ...
 constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least this much
+constexpr int kBackoffCap = 3;       // polish back-off doubles per failed session, up to 8x
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
@@ -1370,6 +1371,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int nfail = 0;          // failed sessions so far (the memory holds the last kFailMem)
   int ntried = 0;         // face sets tried in the current session
   bool seen_start = false;  // the current session started from a remembered failed set
+  int last_pol = 0;       // iteration of the last polish session
   const float alpha = P.alpha;
   if (n == 0) status = 1;
   if (n > 0 && in.w_init != nullptr) {
@@ -1542,9 +1544,13 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #endif
     stable = (__any(changed) != 0) ? 0 : stable + 1;
     bool do_pol = false;
-    if (stable >= P.polish_stable && !last) {
+    // back off before a further attempt, longer after failed sessions: both the stable run and
+    // the distance to the last session grow as polish_stable x 2^min(nfail, kBackoffCap)
+    const int backoff = P.polish_stable << min(nfail, kBackoffCap);
+    if (stable >= P.polish_stable && !last && it - last_pol >= backoff) {
       do_pol = true;
-      stable = -P.polish_stable;  // back off before a further attempt
+      last_pol = it;
+      stable = -backoff;
     }
     if (adapt || last) {
       rp = wave_max(lrp); rd = wave_max(lrd); np_ = wave_max(lnp); nd = wave_max(lnd);

@@ -3,5 +3,5 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 for seed in 11 22 33 44 55; do
-  timeout -k 10 120 python tools/find_stuck.py $seed 2>/dev/null || exit 1
+  timeout -k 10 120 python tools/find_stuck.py $seed $1 2>/dev/null || exit 1
 done

@@ -1,6 +1,6 @@
 """NumPy model of the HIP solver's algorithm (TEST INFRASTRUCTURE).
 
-Mirrors ``convex-mpc-unitree-go2_amd/csrc/cmpc_kernels.hip`` step for step (condensed
+Mirrors ``convex-mpc-unitree-go2_amd/csrc/cmpc_wave.hip`` step for step (condensed
 free-force ADMM with an fp32 preconditioner, accurate error-coordinate gradient, active-set
 polish with iterative refinement) so the algorithm's logic can be exercised on CPU.  Not the
 oracle: the oracle is ``oracle/tight_solver.py``.
@@ -229,7 +229,7 @@ def solve(inst, p: Params):
     g0, _ = gradient(A, B, d, p.Q, p.R, full(x))
     g0 = g0.reshape(-1)[fidx]               # = q of the condensed QP (gradient at 0)
     nq = float(np.max(np.abs(g0), initial=0.0))
-    prev_code = None; stable = 0
+    prev_code = None; stable = 0; last_pol = 0
     status = -2; it = 0; U = None
     for it in range(1, p.max_iter + 1):
         g, _ = gradient(A, B, d, p.Q, p.R, full(x))
@@ -247,7 +247,9 @@ def solve(inst, p: Params):
         else:
             stable = 0
         prev_code = code
-        if stable >= p.stable_checks:
+        backoff = p.stable_checks << min(len(failed_starts), 3)   # cmpc_wave.hip kBackoffCap
+        if stable >= p.stable_checks and it - last_pol >= backoff:
+            last_pol = it
             # a session: polish ADMM's face set, then repair it.  A set that started a failed
             # session before is polished once more without repairs; a repair that returns to a
             # set this session already tried ends the session (cmpc_wave.hip kFailMem/kTryMem).
@@ -264,7 +266,7 @@ def solve(inst, p: Params):
                 tried.append(code.tobytes())
                 ok, u = polish(z, code)
                 rep += 1
-            stable = -p.stable_checks  # back off before the next attempt
+            stable = -backoff  # back off before the next attempt
             if not ok and self_loose[0]:
                 ok = True  # the session ends within the loose tolerance (kLooseTol): accepted
             if ok:

@@ -9,7 +9,10 @@ sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 
 def main():
     import torch
-    from cmpc import Plan, SolverParams, to_device_batch, synth, _lib
+    from cmpc import _lib
+    if len(sys.argv) > 2:  # alternative build
+        _lib._lib = _lib.load(sys.argv[2])
+    from cmpc import Plan, SolverParams, to_device_batch, synth
     seed = 2 + int(sys.argv[1])
     b = synth.make_batch(65536, seed=seed, mixed=True)
     d = to_device_batch(b)
@@ -19,6 +22,7 @@ def main():
     st, it = st.cpu().numpy(), it.cpu().numpy()
     bad = np.nonzero(st != 1)[0]
     print("seed", seed, "not status 1:", bad.tolist(), st[bad].tolist(), it[bad].tolist())
+    print("iterations: mean %.3f sum %d" % (it.mean(), it.sum()))
     top = np.argsort(-it)[:6]
     print("most iterations:", top.tolist(), it[top].tolist())
     np.save(REPO / "gpurun_out/stuck_idx.npy", np.concatenate([bad, top]))
