@@ -57,6 +57,9 @@ __device__ __forceinline__ float dpp(float v) {
 
 // wave-uniform copy of a value the compiler cannot prove uniform (keeps branches scalar)
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uniformf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
+}
 
 // v[l] and v[l ^ 32] (resp. v[l ^ 16]) without address registers (gfx950 permlane swaps):
 // after the swap the two results hold the lane's own value and its partner's in some order
@@ -830,7 +833,7 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
 // held as ONE accumulator tile (lane (g, c): states 4g..4g+3 of step c):
 //   forward  e_{k+1} = sum_j A^{k-j} h_j :   E <- E + A^d shift_d(E),      d = 1, 2, 4, 8
 //   adjoint  lambda_k = sum_j (A')^{j-k} Q2 e_{j+1} : L <- L + (A')^d shift_-d(L)
-// (Hillis-Steele; the step shift is a DPP row shift, the product four MFMAs whose accumulator
+// (Hillis-Steele; the step shift is a DPP row shift, the product three MFMAs whose accumulator
 // is the trajectory itself).  A^d and (A')^d come from repeated squaring in the same layout.
 template <int NC>
 __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, const float* vin,
@@ -1364,7 +1367,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   bool refactor = n > 0;  // (re)build + invert the matrix for the current basis
   bool in_polish = false;
   int nact = n;           // params of the current basis
-  float shift = P.sigma + rho;
+  float shift = uniformf(P.sigma + rho);
   int it = 0;
   int repairs_left = 0;
   bool parked = false;    // the ADMM inverse is in the park slab
@@ -1392,7 +1395,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       ++dg_fact;
 #endif
       CMPC_T0(t_c);
-      condense_tiles<NC>(s, P, M, nact, shift);
+      condense_tiles<NC>(s, P, M, nact, uniformf(shift));
       CMPC_ACC(0, t_c);
       CMPC_T0(t_i);
       invert_tiles<NC>(s, M, nact);
@@ -1472,7 +1475,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       build_admm_basis<NC>(s, P, Bg, ntri);
       in_polish = false;
       nact = n;
-      shift = P.sigma + rho;
+      shift = uniformf(P.sigma + rho);
       if (parked) {
         park_load<NC>(park, M);
       } else {
@@ -1559,8 +1562,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       float q = rho * sqrtf((rp / fmaxf(np_, 1e-30f)) / (rd / fmaxf(nd, 1e-30f) + 1e-30f));
       q = fminf(fmaxf(q, 1e-6f), 1e6f);
       if (q > 5.f * rho || q < 0.2f * rho) {
-        rho = q;
-        shift = P.sigma + rho;
+        rho = uniformf(q);
+        shift = uniformf(P.sigma + rho);
         refactor = true;
       }
     }
