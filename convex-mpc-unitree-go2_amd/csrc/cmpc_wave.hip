@@ -7,12 +7,12 @@
 // flight (2 per SIMD) so one QP's latency is hidden behind another's MFMA/VALU work.
 // Algorithm (DESIGN.md "Kernel"):
 //
-//   1. Condense the horizon onto the free (stance) forces: H = 2 G'QG + 2R via the backward
-//      recursion S_j = Q2 + A'S_{j+1}A, W_jj = S_j B_j, W_ij = A'W_{i+1,j}, H_ij = B_i'W_ij, every
-//      12x12 product a chain of four v_mfma_f32_16x16x4_f32 whose accumulator is the next
-//      product's B operand.  H blocks are scattered into a per-wave global image laid out as the
-//      MFMA accumulator tiles (L2-resident), then loaded back as 16x16 tiles: lane (g, c)
-//      holds rows 4g..4g+3, column c of every lower-triangle tile (f4 per tile, in registers).
+//   1. Condense the horizon onto the free (stance) forces straight into register tiles:
+//      H = sum_t G_t' Q2 G_t + diag(R) + shift with G_t = A G_{t-1} + (step t's new columns),
+//      each product three v_mfma_f32_16x16x4_f32 (K = 12 states) whose accumulator is the
+//      tile itself (condense_tiles_fwd); small batches use the block-row form
+//      H_ij = C_i' A^{i-j} B_j, P_i = Q2 + A'P_{i+1}A (condense_tiles_bc).  Lane (g, c) holds
+//      rows 4g..4g+3, column c of every lower-triangle 16x16 tile (f4 per tile, in registers).
 //   2. Invert H + diag(R) + shift in registers by the BLOCK sweep operator, four pivots at a
 //      time: S <- S - P^ D^-1 P^' (P^ = the four pivot columns with the pivot block minus I),
 //      then -2 on the four pivot diagonals; the rank-4 update of each tile is ONE MFMA
@@ -146,9 +146,19 @@ __device__ __forceinline__ int opaque_lane() {
 // ------------------------------------------------------------------------------------------
 #ifdef CMPC_STAMPS
 __device__ unsigned long long g_stamps[16];
-#define CMPC_T0(name) const unsigned long long name = __builtin_amdgcn_s_memtime()
+// (fenced: outstanding memory and LDS traffic completes, no code moves across a stamp)
+#define CMPC_FENCE()                                            \
+  do {                                                          \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  } while (0)
+#define CMPC_T0(name) \
+  CMPC_FENCE();       \
+  const unsigned long long name = __builtin_amdgcn_s_memtime()
 #define CMPC_ACC(ph, t0)                                                              \
   do {                                                                                \
+    CMPC_FENCE();                                                                     \
     const unsigned long long _t1 = __builtin_amdgcn_s_memtime();                      \
     if (threadIdx.x == 0) atomicAdd(&g_stamps[ph], _t1 - (t0));                       \
   } while (0)
@@ -181,9 +191,8 @@ struct Cfg {
 // Polish sessions and their face sets.  A session starts from ADMM's face set and repairs it
 // (primal-dual active-set steps, one factorization each).  Two memories cut the factorizations
 // that hard instances used to spend on cycling:
-//  * within a session, a repair that returns to a face set the session already tried (the full
-//    primal-dual step cycles) is cut down to the change of the most violated triple alone; if
-//    that set was tried too, the session ends;
+//  * within a session, a repair that returns to a face set the session already tried ends the
+//    session (the repair sequence has entered a cycle);
 //  * a session that ends on a face set whose KKT violations are all within kLooseTol x the
 //    polish tolerance is accepted: a weakly active face at a degenerate vertex can leave every
 //    face set a few 1e-5 relative off in fp32 (the two sets of the cycle straddle it), and
