@@ -334,9 +334,42 @@ def make_qp_fixture(cfg: int, B: int, name: str):
     print(name, B, "instances, max KKT residual", np.max(KKT))
 
 
+# Instances of the cfg2 benchmark batches (synth.make_batch(65536, seed, mixed=True)) that
+# exposed solver weaknesses on the GPU: (seed, index, what happened)
+HARD_CASES = [
+    (57, 1420, "degenerate vertex: two face sets straddle a weakly active friction face, "
+               "neither passed the 1e-5 KKT check in fp32 (status 2 after 1000 iterations)"),
+    (24, 30782, "ill-conditioned face set: refinement contracts ~30x per step, 4 steps were "
+                "not enough (566 iterations)"),
+    (57, 32430, "primal-dual repairs wander between face sets (slowest instance, 273 iterations)"),
+    (46, 18051, "slow ADMM, many polish sessions (227 iterations)"),
+]
+
+
+def make_hard_fixture(name: str = "qp_hard.npz"):
+    rows = {k: [] for k in ("Ad", "Bd", "gd", "x0", "xref", "contact")}
+    W, LX, LA, KKT = [], [], [], []
+    for seed, idx, _ in HARD_CASES:
+        b = synth.make_batch(65536, seed=seed, mixed=True)
+        for k in rows:
+            rows[k].append(b[k][idx])
+        qp = mpc_qp.build_qp(b['Ad'][idx], b['Bd'][idx], b['gd'][idx], b['x0'][idx],
+                             b['xref'][idx].T, b['contact'][idx])
+        r = tight_solver.solve(qp)
+        k = r['kkt']
+        assert max(k.values()) < 1e-8, (seed, idx, k)
+        W.append(r['w']); LX.append(r['lam_x']); LA.append(r['lam_a'])
+        KKT.append([k['stat'], k['prim'], k['comp']])
+    np.savez_compressed(HERE / name, cases=np.array([[s, i] for s, i, _ in HARD_CASES]),
+                        **{k: np.array(v) for k, v in rows.items()}, w=np.array(W),
+                        lam_x=np.array(LX), lam_a=np.array(LA), kkt=np.array(KKT))
+    print(name, len(W), "instances, max KKT residual", np.max(KKT))
+
+
 if __name__ == "__main__":
     make_ref_inputs()
     make_traj_ticks()
     make_leg_ticks()
     make_qp_fixture(1, 32, "qp_cfg1.npz")
     make_qp_fixture(2, 64, "qp_cfg2.npz")
+    make_hard_fixture()

@@ -31,6 +31,23 @@ def test_fixture_parity(plan, name):
     assert feasibility(batch, Ug).max() < 1e-3
 
 
+def test_hard_cases(plan):
+    """Benchmark-batch instances that exposed solver weaknesses (tests/golden/make_golden.py
+    HARD_CASES: a degenerate vertex, an ill-conditioned face set, wandering repairs), each
+    replicated past the latency-mode threshold (B > 4 x CUs) so they run the same arithmetic
+    as in the 65,536-instance batch they came from."""
+    from cmpc import solve_batch
+    fx = load_fixture("qp_hard.npz")
+    reps = 1100
+    batch = {k: np.repeat(v, reps, axis=0) for k, v in fixture_batch(fx).items()}
+    w, st, it = solve_batch(batch, plan=plan)
+    assert np.all(st == 1), [(tuple(c), np.unique(st[i * reps:(i + 1) * reps]).tolist())
+                             for i, c in enumerate(fx["cases"])]
+    err = rel_err_U(w, np.repeat(fx["w"], reps, axis=0))
+    assert err.max() <= TOL_U, (err.max(), int(err.argmax()) // reps)
+    assert it.max() < 400, [int(it[i * reps:(i + 1) * reps].max()) for i in range(len(fx["w"]))]
+
+
 def test_status_and_iters_sane(plan):
     from cmpc import solve_batch, synth
     b = synth.make_config(2, B=4096)

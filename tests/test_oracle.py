@@ -63,10 +63,11 @@ def test_qp_structure_matches_reference_print():
     assert qp["lba"].shape == (448,) and qp["lbx"].shape == (384,)
 
 
-@pytest.mark.parametrize("name", ["qp_cfg1.npz", "qp_cfg2.npz"])
+@pytest.mark.parametrize("name", ["qp_cfg1.npz", "qp_cfg2.npz", "qp_hard.npz"])
 def test_golden_fixtures_are_kkt_certified(name):
     fx = load_fixture(name)
-    for i in range(0, fx["w"].shape[0], 8):
+    n = fx["w"].shape[0]
+    for i in range(0, n, 8 if n > 8 else 1):
         qp = mpc_qp.build_qp(fx["Ad"][i], fx["Bd"][i], fx["gd"][i], fx["x0"][i], fx["xref"][i].T,
                              fx["contact"][i])
         k = mpc_qp.kkt_residuals(qp, fx["w"][i], fx["lam_x"][i], fx["lam_a"][i])
