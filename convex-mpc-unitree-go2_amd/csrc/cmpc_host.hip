@@ -254,7 +254,11 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
   if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   int launched[cmpc::kNumBins] = {0};
-  for (int q = 0; q < cmpc::kNumBins; ++q) {
+  // largest bin first: its persistent waves (one per SIMD at NC >= 160) take the CUs first and
+  // the cheaper bins fill in behind them, so the batch does not end on a late-started big bin
+  // (cfg2 +2-3 %)
+  for (int qi = 0; qi < cmpc::kNumBins; ++qi) {
+    const int q = cmpc::kNumBins - 1 - qi;
     if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) continue;  // bins beyond 12N are empty
     const long long g = pl->grid[q] < B ? pl->grid[q] : B;
     hipStream_t bs = pl->bin_stream[q];
