@@ -146,7 +146,8 @@ __device__ __forceinline__ int opaque_lane() {
 // ------------------------------------------------------------------------------------------
 #ifdef CMPC_STAMPS
 __device__ unsigned long long g_stamps[16];
-// (fenced: outstanding memory and LDS traffic completes, no code moves across a stamp)
+// (fenced: outstanding memory and LDS traffic completes, no code moves across a stamp; totals
+// accumulate per wave in LDS, so no contended atomic sits between two stamps)
 #define CMPC_FENCE()                                            \
   do {                                                          \
     __builtin_amdgcn_sched_barrier(0);                          \
@@ -160,10 +161,10 @@ __device__ unsigned long long g_stamps[16];
   do {                                                                                \
     CMPC_FENCE();                                                                     \
     const unsigned long long _t1 = __builtin_amdgcn_s_memtime();                      \
-    if (threadIdx.x == 0) atomicAdd(&g_stamps[ph], _t1 - (t0));                       \
+    if (threadIdx.x == 0) s.st[ph] += _t1 - (t0);                                     \
   } while (0)
 #define CMPC_CNT(ph, v) \
-  do { if (threadIdx.x == 0) atomicAdd(&g_stamps[ph], (unsigned long long)(v)); } while (0)
+  do { if (threadIdx.x == 0) s.st[ph] += (unsigned long long)(v); } while (0)
 #else
 #define CMPC_T0(name) (void)0
 #define CMPC_ACC(ph, t0) (void)0
@@ -212,6 +213,9 @@ constexpr float kLooseTol = 5.f;
 
 template <int NC>
 struct Smem {
+#ifdef CMPC_STAMPS
+  unsigned long long st[16];       // per-wave stamp totals (flushed to g_stamps at exit)
+#endif
   alignas(16) float Bt[NC * 12];   // param-space input matrix, column p at Bt[12p .. 12p+11]
   alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
   alignas(16) float x[NC];
@@ -1662,6 +1666,9 @@ __global__ void __launch_bounds__(64, Cfg<NC>::WPE)
     s.R2[lane] = P.R2[lane];
   }
   const int total = *count;
+#ifdef CMPC_STAMPS
+  if (lane < 16) s.st[lane] = 0;
+#endif
   for (;;) {
     int idx = 0;
     if (lane == 0) idx = atomicAdd(head, 1);
@@ -1669,6 +1676,10 @@ __global__ void __launch_bounds__(64, Cfg<NC>::WPE)
     if (idx >= total) break;
     solve_instance<NC>(s, P, (int64_t)list[idx], in, out, park);
   }
+#ifdef CMPC_STAMPS
+  WSYNC();
+  if (lane < 16) atomicAdd(&g_stamps[lane], s.st[lane]);
+#endif
 }
 
 __global__ void __launch_bounds__(256) bin_kernel(int N, int64_t B,
