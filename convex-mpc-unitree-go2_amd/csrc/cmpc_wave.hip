@@ -42,6 +42,7 @@ namespace cmpc {
 #endif
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------------
 // wave helpers
@@ -808,19 +809,24 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
     f4 xr = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
 #pragma unroll
     for (int q = 0; q < 4; ++q) xr[q] = (16 * I + 4 * g + q < n) ? xr[q] : 0.f;
-    f4 racc = {0.f, 0.f, 0.f, 0.f};
+    // packed f32 FMAs (v_pk_fma_f32, the broadcast operand by op_sel): two of the four rows
+    // per instruction
+    f2 r01 = {0.f, 0.f}, r23 = {0.f, 0.f};
+    const f2 x01 = {xr[0], xr[1]}, x23 = {xr[2], xr[3]};
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
       const f4 m = M[tile_index(I, J)];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) racc[q] = fmaf(m[q], xc[J], racc[q]);
+      const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
+      const f2 xj = {xc[J], xc[J]};
+      r01 = __builtin_elementwise_fma(m01, xj, r01);
+      r23 = __builtin_elementwise_fma(m23, xj, r23);
       if (J < I) {
-        float cs = cacc[J];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cs = fmaf(m[q], xr[q], cs);
-        cacc[J] = cs;
+        f2 cp = m01 * x01;
+        cp = __builtin_elementwise_fma(m23, x23, cp);
+        cacc[J] += cp[0] + cp[1];
       }
     }
+    const f4 racc = {r01[0], r01[1], r23[0], r23[1]};
     // row sums over the 16 lanes of each DPP row -> out rows 16I + 4g + q
     f4 rs;
 #pragma unroll
