@@ -952,14 +952,14 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
     const int k = s.par[p];
     const f4* bt = reinterpret_cast<const f4*>(&s.Bt[p * 12]);
     const f4* l = reinterpret_cast<const f4*>(&s.L[12 * k]);
-    float acc = s.Rt[p] * vin[p];
+    f2 a2 = {s.Rt[p] * vin[p], 0.f};  // packed: even and odd states in the two halves
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const f4 lv = l[j], bv = bt[j];
-      acc = fmaf(bv[0], lv[0], acc); acc = fmaf(bv[1], lv[1], acc);
-      acc = fmaf(bv[2], lv[2], acc); acc = fmaf(bv[3], lv[3], acc);
+      a2 = __builtin_elementwise_fma(f2{bv[0], bv[1]}, f2{lv[0], lv[1]}, a2);
+      a2 = __builtin_elementwise_fma(f2{bv[2], bv[3]}, f2{lv[2], lv[3]}, a2);
     }
-    gout[p] = acc;
+    gout[p] = a2[0] + a2[1];
   }
   WSYNC();
   CMPC_ACC(2, t_gr);
