@@ -1,4 +1,5 @@
-"""Diagnostic: instances of a cfg2 batch (seed offset argv[1]) that reach max_iter, with their
+"""Diagnostic: instances of a cfg batch (seed offset argv[1], lib argv[2], config argv[3],
+default 2) that do not reach status 1, with their
 iteration / polish-session / factorization counts (product and diag builds)."""
 import sys
 from pathlib import Path
@@ -13,8 +14,9 @@ def main():
     if len(sys.argv) > 2:  # alternative build
         _lib._lib = _lib.load(sys.argv[2])
     from cmpc import Plan, SolverParams, to_device_batch, synth
-    seed = 2 + int(sys.argv[1])
-    b = synth.make_batch(65536, seed=seed, mixed=True)
+    cfg = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    seed = synth.CONFIGS[cfg]["seed"] + int(sys.argv[1])
+    b = synth.make_batch(65536, seed=seed, mixed=synth.CONFIGS[cfg]["mixed"])
     d = to_device_batch(b)
     plan = Plan(SolverParams(max_batch=65536))
     w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
