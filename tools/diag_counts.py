@@ -10,6 +10,14 @@ REPO = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 
 
+def _lpt(cyc, W):
+    import heapq
+    h = [0.0] * W
+    for cv in np.sort(cyc)[::-1]:
+        heapq.heappush(h, heapq.heappop(h) + cv)
+    return max(h)
+
+
 def main():
     import torch
     from cmpc import _lib
@@ -40,6 +48,16 @@ def main():
         print(f"  max: cycles {cyc.max():.0f} iters {iters[order[0]]} polish {pol[order[0]]} fact {fac[order[0]]}")
         for q in (50, 90, 99, 99.9):
             print(f"  p{q}: cycles {np.percentile(cyc, q):.0f} iters {np.percentile(iters, q):.0f} fact {np.percentile(fac, q):.0f}")
+        if cfg == 1:  # one bin: persistent waves pulling the queue in (about) index order
+            import heapq
+            W = 2048  # 8 waves per CU x 256 CUs (NC = 128)
+            h = [0.0] * W
+            for cv in cyc:
+                heapq.heappush(h, heapq.heappop(h) + cv)
+            ideal = cyc.sum() / W
+            print(f"  queue drain model: makespan {max(h):.0f} vs even share {ideal:.0f} cycles "
+                  f"-> tail {100 * (max(h) / ideal - 1):.1f} %; sorted hardest-first "
+                  f"{100 * (_lpt(cyc, W) / ideal - 1):.1f} %")
 
 
 if __name__ == "__main__":
