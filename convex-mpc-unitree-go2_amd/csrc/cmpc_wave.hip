@@ -208,6 +208,7 @@ struct Cfg {
 constexpr int kRefineExtra = 4;      // polish refinements beyond polish_refine ...
 constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least this much
 constexpr int kBackoffCap = 3;       // polish back-off doubles per failed session, up to 8x
+constexpr int kLateRepairs = 3;      // repair budget of the sessions after two failed ones
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
@@ -1248,7 +1249,10 @@ __device__ __forceinline__ int session_start(Smem<NC>& s, const KParams& P, int 
     const bool diff = (l < ntri) && (s.fpat[k][l] != c);
     seen |= (__any(diff) == 0);
   }
-  return seen ? 0 : P.polish_repairs;
+  if (seen) return 0;
+  // after two failed sessions the repair budget shrinks: a wandering repair sequence costs a
+  // factorization per step (cfg1 +1 %, cfg2 +1-2 %)
+  return (nfail >= 2) ? min(P.polish_repairs, kLateRepairs) : P.polish_repairs;
 }
 
 // Has the current session already tried the repaired face set in s.tcnt?

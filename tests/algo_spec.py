@@ -258,7 +258,8 @@ def solve(inst, p: Params):
             tried = [start]
             ok, u = polish(z, code)
             rep = 0
-            while not ok and rep < (0 if seen else p.repairs):
+            budget = 0 if seen else (min(p.repairs, 3) if len(failed_starts) >= 2 else p.repairs)
+            while not ok and rep < budget:   # cmpc_wave.hip kLateRepairs
                 c2 = self_newcode[0]
                 if np.array_equal(c2, code) or c2.tobytes() in tried[:8]:
                     break
