@@ -67,7 +67,8 @@ typedef struct cmpc_params {
   float eps_abs;          /* ADMM residual tolerances for status 2 (OPTS eps_abs/eps_rel) */
   float eps_rel;
   int32_t max_iter;       /* ADMM iteration cap (OPTS max_iter) */
-  float rho;              /* initial ADMM penalty */
+  float rho;              /* initial ADMM penalty (the NC = 128 bin starts at rho / 2 and returns
+                             to rho after a failed polish session) */
   float sigma;            /* ADMM proximal regularisation (OSQP sigma) */
   float alpha;            /* over-relaxation (OSQP alpha) */
   int32_t adaptive_rho_interval; /* iterations between rho updates (0 = off) */

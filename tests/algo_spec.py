@@ -223,7 +223,10 @@ def solve(inst, p: Params):
     self_loose = [False]
 
     failed_starts = []
-    rho = p.rho
+    # the NC = 128 bin (96 < nf <= 128) starts from rho / 2 and returns to rho after its first
+    # failed polish session (cmpc_wave.hip solve_instance, rho_low)
+    rho_low = 96 < nf <= 128
+    rho = p.rho * (0.5 if rho_low else 1.0)
     L = admm_matrix(rho)
     x = np.zeros(nf, F32); z = np.zeros(nf, F32); y = np.zeros(nf, F32)
     g0, _ = gradient(A, B, d, p.Q, p.R, full(x))
@@ -274,6 +277,8 @@ def solve(inst, p: Params):
                 status = 1; U = u; break
             if not seen:
                 failed_starts.append(start)
+            if rho_low:
+                rho_low = False; rho = p.rho; L = admm_matrix(rho)
         if p.adaptive_interval and it % p.adaptive_interval == 0:
             rp = np.max(np.abs(x - z)); rd = np.max(np.abs(g + y))
             npn = max(np.max(np.abs(x)), np.max(np.abs(z)), 1e-30)
@@ -282,7 +287,7 @@ def solve(inst, p: Params):
             nr = rho * np.sqrt((rp / npn) / (rd / nd + 1e-30))
             nr = min(max(nr, 1e-6), 1e6)
             if nr > 5 * rho or nr < rho / 5:
-                rho = nr; L = admm_matrix(rho)
+                rho = nr; L = admm_matrix(rho); rho_low = False
     if U is None:
         U = full(z).reshape(-1)
     return dict(U=U.reshape(N, 12), status=status, iters=it, nf=nf)
