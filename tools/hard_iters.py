@@ -1,3 +1,5 @@
+"""Diagnostic: status and max iterations of the hard-case fixture (tests/golden/qp_hard.npz,
+each instance replicated 1,100x) under a given build: python tools/hard_iters.py <lib.so>."""
 import sys, numpy as np
 sys.path.insert(0, 'convex-mpc-unitree-go2_amd'); sys.path.insert(0, 'tests')
 import torch
