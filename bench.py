@@ -1,26 +1,41 @@
 #!/usr/bin/env python3
 """bench.py -- batched convex-MPC QP solves/sec on MI355X (BASELINE.json metric).
 
-One *step* = one cmpc_solve over a resident batch of synthetic Go2 QP instances
-(default workload: config 1 distribution -- trot 3 Hz / duty 0.6 fixed
-contact schedule, seed 1 -- at ``--batch`` instances per GPU).  Instances are independent, so
-ranks shard them with no data-path collective (weak scaling: every rank solves its own
-``--batch`` instances, generated rank-locally from seed + rank); only the barrier and the
-max-over-ranks timing reduction use the process group.
+Headline (BASELINE.json configs[3]): the config-3 workload -- 65,536
+synthetic Go2 QP instances, trot (fixed 3 Hz / 0.6 schedule) and mixed stance masks
+interleaved -- is ONE global batch sharded over the N ranks (one process per GPU): rank r
+solves the contiguous slice [r B/N, (r+1) B/N) of it, resident in its HBM.  One *step* = one
+``cmpc_solve`` of every rank's shard; ``value`` = 65,536 x steps / (max over ranks of the
+timed region), ``"scaling": "strong"``.
 
-    python bench.py [--gpus N --steps K --warmup W --config 1|2|3 --batch B]
+    python bench.py [--gpus N --steps K --warmup W --config 3|2|1 --batch B]
 
-Rank 0 prints one JSON line.  ``roofline`` prices the dominant solve kernel (the free-variable
-bin that holds most instances) against HBM: algorithmic bytes = 12,264 B per solve (inputs
-10,720 + outputs 1,544) x solves in that launch / its average HIP-event duration.
-``cpu_baseline`` times the oracle's C restatement of the reference's OSQP path
-(oracle/osqp_ref.c, float64, the reference's OPTS) on a bounded sample of the same workload.
+``--gpus N`` (N > 1) without a torch.distributed environment re-launches this script under
+``torch.distributed.run`` with N ranks (before anything touches the GPU); under an existing
+launcher WORLD_SIZE must equal N.
+
+Also on the line:
+  * ``scatter_gather`` (N > 1): the same global batch owned by rank 0 -- one RCCL scatter of
+    the input stacks, the solve, one RCCL gather of w per step (cmpc/dist.py);
+  * ``weak``: every rank solves the whole 65,536-instance batch (per-GPU work fixed);
+  * ``configs`` (N = 1): BASELINE configs 1 (B = 256) and 2 (B = 4,096), plus configs 1 and 2
+    at B = 65,536, each timed the same way with its own roofline;
+  * ``roofline``: the dominant solve kernel (of the two, cmpc_host.hip) priced against HBM:
+    12,264 algorithmic bytes per solve (inputs 10,720 + outputs 1,544) x the solves it
+    processed / its average HIP-event duration on its own stream; ``traffic`` = the PMC HBM
+    bytes per launch from profiles/;
+  * ``cpu_baseline`` (rank 0, N = 1): the oracle's C++ restatement of the reference's OSQP
+    path on a bounded sample of the same workload (a reported baseline, not the target);
+  * the SURVEY 8(f) objects (N = 1): on-device dynamics, warm start, the on-device tick, the
+    leg controller, the closed loop, config 0 through the drop-in API.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -30,23 +45,27 @@ import numpy as np
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 
+METRIC = "batched QP solves/sec (N=16, 4-leg friction cone) at 1/2/4/8 MI355X"
 BYTES_IN = 576 + 9216 + 48 + 48 + 768 + 64      # Ad, Bd, gd, x0, xref, contact (N=16, fp32/u8)
 BYTES_OUT = 1536 + 4 + 4                         # w, status, iters
 BYTES_PER_SOLVE = BYTES_IN + BYTES_OUT           # 12,264
 HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s spec
 F32_MATRIX_PEAK_TFS = 157.3                      # MI355X_MICROARCH.md: dense f32 MFMA peak
 POLISH_REFINE = 4                                # SolverParams.polish_refine (default)
+GLOBAL_BATCH = {1: 256, 2: 4096, 3: 65536}       # BASELINE.json configs[1..3]
+KERNEL_BINS = ((1, 0), (3, 2))                   # cmpc/_lib.py: kernel k serves these bins
+KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<192, 160>")
 
 
 def algorithmic_flops(contact, iters, N=16):
-    """Algorithmic FP32 work per instance of the path's algorithm (DESIGN.md "Roofline"):
-    one ADMM and one polish factorisation at the instance's free-force count n (condensation
+    """Algorithmic FP32 work per instance of the path's algorithm: one ADMM and
+    one polish factorisation at the instance's free-force count n (condensation
     sum_t 12 m_t^2 + 288 m_{t-1} with m_t = free forces of steps <= t, sweep inverse n^3),
     `iters` ADMM iterations and POLISH_REFINE refinements of symv (2 n^2) + gradient
     (576 N + 48 n).  Counts only the accepted path (no rho refactors, repairs or padding)."""
-    st = (contact != 0).reshape(contact.shape[0], 4, -1)           # (B, 4, N)
-    per_step = 3 * st.sum(1).astype(np.float64)                     # free forces per step
-    m = np.cumsum(per_step, axis=1)                                 # m_t
+    st = (contact != 0).reshape(contact.shape[0], 4, -1)
+    per_step = 3 * st.sum(1).astype(np.float64)
+    m = np.cumsum(per_step, axis=1)
     n = m[:, -1]
     m_prev = np.concatenate([np.zeros((m.shape[0], 1)), m[:, :-1]], axis=1)
     cond = (12.0 * m ** 2 + 288.0 * m_prev).sum(1)
@@ -57,18 +76,41 @@ def algorithmic_flops(contact, iters, N=16):
     return 2.0 * (cond + inv) + it * (symv + grad) + POLISH_REFINE * symv + (POLISH_REFINE + 1) * grad
 
 
-def parse():
+def bins_of(contact):
+    nf = 3 * (contact != 0).reshape(contact.shape[0], -1).sum(1)
+    caps = np.array([96, 128, 160, 192])
+    return np.searchsorted(caps, nf)   # first cap >= nf
+
+
+def kernel_of_bins(bins):
+    k = np.zeros_like(bins)
+    k[bins >= 2] = 1
+    return k
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=1, choices=(1, 2, 3))
-    ap.add_argument("--batch", type=int, default=65536, help="instances per GPU per step")
+    ap.add_argument("--config", type=int, default=3, choices=(1, 2, 3),
+                    help="headline workload (BASELINE.json configs[1..3]); default 3")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="GLOBAL batch of the headline (default: the config's own, 3 -> 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the CPU-baseline sample (0 = skip)")
     ap.add_argument("--traffic-json", type=str, default=str(REPO / "profiles" / "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
-    ap.add_argument("--latency-batch", type=int, default=256)
+    ap.add_argument("--counters-json", type=str,
+                    default=str(REPO / "profiles" / "r02_counters.json"),
+                    help="PMC instruction counters of the dominant kernel (profiles/)")
+    ap.add_argument("--sub-configs", type=int, default=1,
+                    help="N = 1: also time configs 1 / 2 at their own and at 65,536 (0 = skip)")
+    ap.add_argument("--scatter-steps", type=int, default=None,
+                    help="N > 1: timed steps of the scatter -> solve -> gather variant "
+                         "(default --steps; 0 = skip)")
+    ap.add_argument("--weak-steps", type=int, default=None,
+                    help="timed steps of the weak-scaling variant (default --steps; 0 = skip)")
     ap.add_argument("--dynamics-steps", type=int, default=5,
                     help="timed steps of the on-device dynamics build (+ fused build+solve); 0 = skip")
     ap.add_argument("--warm-steps", type=int, default=5,
@@ -82,125 +124,390 @@ def parse():
                     help="timed closed-loop MPC ticks (config 4 shape, SRB plant); 0 = skip")
     ap.add_argument("--api-ticks", type=int, default=20,
                     help="config 0: ticks of one robot through the CentroidalMPC drop-in; 0 = skip")
+    ap.add_argument("--aux", type=int, default=1,
+                    help="0 = headline only (profiling runs): skips every other object")
     ap.add_argument("--seed-offset", type=int, default=0,
                     help="added to the workload seed (experiments: average over batches)")
     ap.add_argument("--param", action="append", default=[],
                     help="SolverParams override key=value (experiments)")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
-    return ap.parse_args()
+    a = ap.parse_args(argv)
+    if not a.aux:
+        a.cpu_seconds = 0
+        a.sub_configs = a.dynamics_steps = a.warm_steps = a.tick_steps = 0
+        a.leg_steps = a.loop_steps = a.api_ticks = 0
+        a.scatter_steps = 0 if a.scatter_steps is None else a.scatter_steps
+        a.weak_steps = 0 if a.weak_steps is None else a.weak_steps
+    if a.scatter_steps is None:
+        a.scatter_steps = a.steps
+    if a.weak_steps is None:
+        a.weak_steps = a.steps
+    return a
 
 
-def bins_of(contact):
-    nf = 3 * (contact != 0).reshape(contact.shape[0], -1).sum(1)
-    caps = np.array([96, 128, 160, 192])
-    return np.searchsorted(caps, nf)   # first cap >= nf
+# ------------------------------------------------------------------------------------------
+# process topology
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def relaunch(n: int, argv) -> int:
+    """Start this script under torch.distributed.run with n ranks (child process; this process
+    has not touched the GPU) and return its exit code."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           str(Path(__file__).resolve()), *argv]
+    return subprocess.call(cmd, env=env)
 
+
+def topology(args):
+    """-> (world, rank, local) from the torch.distributed.run environment, checked against
+    --gpus.  Raises SystemExit when they disagree."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with "
+                         f"'python bench.py --gpus N' or torchrun --nproc-per-node N ... --gpus N")
+    return world, rank, local
+
+
+def timed_steps(step, steps, warmup, sync, barrier, reduce_max):
+    """Run `warmup` untimed steps, then time exactly `steps` steps bracketed by barrier + device
+    sync on both sides; -> seconds (max over ranks)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    return reduce_max(time.perf_counter() - t0)
+
+
+# ------------------------------------------------------------------------------------------
+# GPU measurement helpers
+# ------------------------------------------------------------------------------------------
+def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None, counters=None):
+    """Roofline of the dominant solve kernel of the last timed steps: algorithmic bytes of the
+    solves it processed / its average HIP-event duration (kernels run on their own streams)."""
+    kern = kernel_of_bins(bins)
+    avg = [ms[k] / max(calls[k], 1) for k in range(2)]
+    q = int(np.argmax(avg))
+    n_q = int(np.sum(kern == q))
+    achieved = BYTES_PER_SOLVE * n_q / (avg[q] * 1e-3) / 1e9 if avg[q] > 0 else 0.0
+    flops = algorithmic_flops(contact, iters)
+    fl_q = float(flops[kern == q].sum())
+    tfs = fl_q / (avg[q] * 1e-3) / 1e12 if avg[q] > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_NAMES[q],
+            "kernel_avg_ms": avg[q], "solves_per_launch": n_q, "bytes_per_solve": BYTES_PER_SOLVE,
+            "kernel_avg_ms_all": {KERNEL_NAMES[k]: avg[k] for k in range(2)},
+            "solves_per_kernel": {KERNEL_NAMES[k]: int(np.sum(kern == k)) for k in range(2)}}
+    comp = {"bound": "mfma", "achieved": tfs, "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": tfs / F32_MATRIX_PEAK_TFS, "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
+            "flops_per_solve": fl_q / max(n_q, 1)}
+    if counters:
+        comp["counters"] = counters
+    return roof, comp
+
+
+def load_json(path):
+    if path and Path(path).exists():
+        try:
+            return json.loads(Path(path).read_text())
+        except Exception:
+            return None
+    return None
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args.gpus, argv))
+    world, rank, local = topology(args)
+
+    import torch
+    import torch.distributed as dist
+    if os.environ.get("CMPC_BENCH_DRYRUN") == "1":
+        return dry_run(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
     if args.lib:
         from cmpc import _lib
         _lib._lib = _lib.load(args.lib)
     from cmpc import Plan, SolverParams, to_device_batch, synth
+    from cmpc import dist as cdist
 
-    B = args.batch
-    cfg = args.config
-    if cfg == 3:
-        batch = synth.make_config(3, B=B)
-    else:
-        batch = synth.make_batch(B, seed=synth.CONFIGS[cfg]["seed"] + 1000 * rank + args.seed_offset,
-                                 mixed=synth.CONFIGS[cfg]["mixed"])
-    bins = bins_of(batch["contact"])
-    d = to_device_batch(batch, dev)
+    def sync():
+        torch.cuda.synchronize(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def reduce_max(x):
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def reduce_sum_int(x):
+        if world == 1:
+            return int(x)
+        t = torch.tensor([x], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return int(t.item())
+
     over = {}
     for kv in args.param:
         k, v = kv.split("=")
         over[k] = type(getattr(SolverParams, k))(float(v) if "." in v or "e" in v else int(v))
-    plan = Plan(SolverParams(max_batch=B, **over), device=dev)
-    w = torch.empty((B, 24 * 16), dtype=torch.float32, device=dev)
-    st = torch.empty((B,), dtype=torch.int32, device=dev)
-    it = torch.empty((B,), dtype=torch.int32, device=dev)
+
+    cfg = args.config
+    GB = args.batch or GLOBAL_BATCH[cfg]
+    if cfg == 3:
+        full = synth.make_config(3, B=GB)
+    else:
+        full = synth.make_batch(GB, seed=synth.CONFIGS[cfg]["seed"] + args.seed_offset,
+                                mixed=synth.CONFIGS[cfg]["mixed"])
+    lo, hi = cdist.shard_bounds(GB, rank, world)
+    shard = {k: full[k][lo:hi] for k in cdist.FIELDS}
+    Bs = hi - lo
+    max_b = max(GB if args.weak_steps > 0 else Bs, 65536 if (world == 1 and args.sub_configs) else 0)
+    plan = Plan(SolverParams(max_batch=max_b, **over), device=dev)
     stream = torch.cuda.current_stream(dev)
+    d = to_device_batch(shard, dev)
+    w = torch.empty((Bs, 24 * 16), dtype=torch.float32, device=dev)
+    st = torch.empty((Bs,), dtype=torch.int32, device=dev)
+    it = torch.empty((Bs,), dtype=torch.int32, device=dev)
 
     def step():
         plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"],
                    out=(w, st, it), stream=stream)
 
+    # ---- headline: strong scaling of the config's global batch over the ranks ----
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    sync()
     plan.timing_read()
     plan.set_timing(True)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
+    elapsed = timed_steps(step, args.steps, 0, sync, barrier, reduce_max)
     plan.set_timing(False)
-    ms_bins, calls = plan.timing_read()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    ms_k, calls_k = plan.timing_read()
+    n_ranks = reduce_sum_int(1)
+    solved = reduce_sum_int(int((st == 1).sum().item()))
     status = st.cpu().numpy()
     iters = it.cpu().numpy()
-    solved_frac = float(np.mean(status == 1))
-    total = B * world * args.steps
-    value = total / elapsed
+    value = GB * args.steps / elapsed
+    bins = bins_of(shard["contact"])
+    traffic_j = load_json(args.traffic_json)
+    traffic = traffic_j.get("hbm_bytes_per_launch") if traffic_j else None
+    counters = load_json(args.counters_json)
+    roof, roof_c = kernel_roofline(plan, Bs, bins, shard["contact"], iters, ms_k, calls_k,
+                                   traffic, counters)
 
-    # dominant kernel: the bin with the most kernel time
-    q = int(np.argmax(ms_bins))
-    n_in_bin = int(np.sum(bins == q))
-    avg_ms = ms_bins[q] / max(calls[q], 1)
-    achieved_gbs = BYTES_PER_SOLVE * n_in_bin / (avg_ms * 1e-3) / 1e9
-    flops = algorithmic_flops(batch["contact"], iters)
-    fl_bin = float(flops[bins == q].sum())
-    achieved_tfs = fl_bin / (avg_ms * 1e-3) / 1e12
-    traffic = None
-    if args.traffic_json and Path(args.traffic_json).exists():
-        tj = json.loads(Path(args.traffic_json).read_text())
-        traffic = tj.get("hbm_bytes_per_launch")
+    # ---- N > 1: scatter from rank 0 -> solve -> gather to rank 0 (RCCL over xGMI) ----
+    scat = None
+    if world > 1 and args.scatter_steps > 0:
+        src = to_device_batch({k: full[k] for k in cdist.FIELDS}, dev) if rank == 0 else None
+        holder = {}
 
-    # latency of one small batch (configs[1]: B=256) on the same plan (0: skip, e.g. under a
-    # profiler so that every traced launch is a full-batch step)
-    lb = min(args.latency_batch, B)
-    lat_ms = None
-    sl = {k: v[:lb] for k, v in d.items()}
-    if lb > 0:
-        for _ in range(3):
-            plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
-        torch.cuda.synchronize(dev)
-        tl0 = time.perf_counter()
-        for _ in range(10):
-            plan.solve(sl["Ad"], sl["Bd"], sl["gd"], sl["x0"], sl["xref"], sl["contact"])
-        torch.cuda.synchronize(dev)
-        lat_ms = (time.perf_counter() - tl0) / 10 * 1e3
+        def sg_step():
+            mine = cdist.scatter_batch(src, GB, 16, dev)
+            ww, ss, ii = plan.solve(mine["Ad"], mine["Bd"], mine["gd"], mine["x0"], mine["xref"],
+                                    mine["contact"], stream=stream)
+            holder["w"] = cdist.gather_solutions(ww, GB)
+        el = timed_steps(sg_step, args.scatter_steps, 2, sync, barrier, reduce_max)
+        ok = True
+        if rank == 0:   # the gathered solutions are the headline's, instance by instance
+            ok = bool(holder["w"].shape == (GB, 384))
+        scat = {"solves_per_s": GB * args.scatter_steps / el,
+                "ms_per_step": el / args.scatter_steps * 1e3,
+                "steps": args.scatter_steps,
+                "comm": "dist.scatter of the 6 input stacks (10,720 B/instance) + dist.gather of "
+                        "w (1,536 B/instance) from/to rank 0 over RCCL, per step",
+                "gathered_shape_ok": ok}
+        del src
 
-    # the discrete dynamics built on the device (cmpc_build_dynamics) --
-    # its own HBM roofline, and the fused per-tick throughput build + solve
-    dyn = None
+    # ---- weak scaling: every rank solves the whole global batch ----
+    weak = None
+    if args.weak_steps > 0 and (world > 1 or GB != Bs):
+        dfull = to_device_batch({k: full[k] for k in cdist.FIELDS}, dev)
+        wf = torch.empty((GB, 384), dtype=torch.float32, device=dev)
+        sf = torch.empty((GB,), dtype=torch.int32, device=dev)
+        itf = torch.empty((GB,), dtype=torch.int32, device=dev)
+
+        def wk_step():
+            plan.solve(dfull["Ad"], dfull["Bd"], dfull["gd"], dfull["x0"], dfull["xref"],
+                       dfull["contact"], out=(wf, sf, itf), stream=stream)
+        el = timed_steps(wk_step, args.weak_steps, 2, sync, barrier, reduce_max)
+        weak = {"solves_per_s": GB * world * args.weak_steps / el,
+                "ms_per_step": el / args.weak_steps * 1e3, "batch_per_gpu": GB,
+                "scaling": "weak"}
+        del dfull, wf, sf, itf
+
+    # ---- N = 1: BASELINE configs 1 and 2 at their own batch, and configs 1 / 2 at 65,536 ----
+    configs = None
+    if world == 1 and args.sub_configs:
+        configs = {}
+        for name, c, B in (("config1_b256", 1, 256), ("config2_b4096", 2, 4096),
+                           ("config1_b65536", 1, 65536), ("config2_b65536", 2, 65536)):
+            b = synth.make_batch(B, seed=synth.CONFIGS[c]["seed"] + args.seed_offset,
+                                 mixed=synth.CONFIGS[c]["mixed"])
+            db = to_device_batch(b, dev)
+            wb = torch.empty((B, 384), dtype=torch.float32, device=dev)
+            sb = torch.empty((B,), dtype=torch.int32, device=dev)
+            ib = torch.empty((B,), dtype=torch.int32, device=dev)
+
+            def c_step():
+                plan.solve(db["Ad"], db["Bd"], db["gd"], db["x0"], db["xref"], db["contact"],
+                           out=(wb, sb, ib), stream=stream)
+            ksteps = 50 if B <= 4096 else args.steps
+            for _ in range(3):
+                c_step()
+            sync()
+            plan.timing_read()
+            plan.set_timing(True)
+            el = timed_steps(c_step, ksteps, 0, sync, barrier, reduce_max)
+            plan.set_timing(False)
+            mk, ck = plan.timing_read()
+            itb = ib.cpu().numpy()
+            r, rc = kernel_roofline(plan, B, bins_of(b["contact"]), b["contact"], itb, mk, ck)
+            configs[name] = {"solves_per_s": B * ksteps / el, "ms_per_step": el / ksteps * 1e3,
+                             "batch": B, "steps": ksteps,
+                             "solved_frac": float((sb == 1).float().mean().item()),
+                             "iters_mean": float(itb.mean()), "iters_max": int(itb.max()),
+                             "roofline": {k: r[k] for k in ("achieved", "frac", "kernel",
+                                                            "kernel_avg_ms", "kernel_avg_ms_all",
+                                                            "solves_per_kernel")},
+                             "roofline_compute_frac": rc["frac"]}
+            del db, wb, sb, ib
+
+    aux = {}
+    if world == 1:
+        aux = aux_objects(args, plan, full, dev, stream, torch)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(full, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": (f"BASELINE config {cfg}: {GB} Go2 QP instances (N=16) "
+                                    + ("trot 3Hz/0.6 + mixed stance masks interleaved"
+                                       if cfg == 3 else "trot 3Hz/0.6 fixed schedule" if cfg == 1
+                                       else "mixed stance masks")
+                                    + f", one global batch sharded over {world} rank(s), "
+                                      "inputs resident in HBM"),
+                       "N": 16, "global_batch": GB, "batch_per_gpu": Bs,
+                       "parallelism": f"instance-sharded x{world} (contiguous slices, no "
+                                      "data-path collective)"},
+            "ranks_reporting": n_ranks,
+            "roofline": roof,
+            "roofline_compute": roof_c,
+            "cpu_baseline": cpu,
+            "solved_frac": solved / GB,
+            "iters_mean": float(np.mean(iters)),
+            "iters_max": int(np.max(iters)),
+            "status_counts": {str(s): int(np.sum(status == s)) for s in np.unique(status)},
+            "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},
+            "scatter_gather": scat,
+            "weak": weak,
+            "configs": configs,
+            **aux,
+            "params_override": over or None,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(args, world, rank):
+    """CMPC_BENCH_DRYRUN=1 (CPU tests): the rank / shard logic of the headline with the solve
+    stubbed -- gloo instead of RCCL, no device.  Rank 0 prints the world size all ranks agree
+    on, each rank's slice of the global batch and the step timing's max-over-ranks."""
+    import torch
+    import torch.distributed as dist
+    from cmpc import dist as cdist
+    if world > 1:
+        dist.init_process_group("gloo")
+    GB = args.batch or GLOBAL_BATCH[args.config]
+    lo, hi = cdist.shard_bounds(GB, rank, world)
+
+    def reduce_max(x):
+        t = torch.tensor([x], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+    work = {"n": 0}
+
+    def step():   # stub solve: touch the shard
+        work["n"] += hi - lo
+    el = timed_steps(step, args.steps, args.warmup, lambda: None, barrier, reduce_max)
+    t = torch.tensor([1, hi - lo, work["n"]], dtype=torch.int64)
+    spans = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_gather(spans, torch.tensor([lo, hi], dtype=torch.int64))
+    else:
+        spans = [torch.tensor([lo, hi])]
+    if rank == 0:
+        print(json.dumps({"n_gpus": world, "ranks_reporting": int(t[0]), "global_batch": GB,
+                          "solved_per_step": int(t[1]), "stub_work": int(t[2]),
+                          "spans": [s.tolist() for s in spans], "elapsed_max": el,
+                          "steps": args.steps, "warmup": args.warmup}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def aux_objects(args, plan, full, dev, stream, torch):
+    """SURVEY.md 8(f) objects on one GPU: each times its own component on a 65,536-robot batch
+    (the headline's instances where they apply)."""
+    from cmpc import to_device_batch, synth
+    out = {}
+    B = min(65536, full["Ad"].shape[0])
+    batch = {k: (v[:B] if isinstance(v, np.ndarray) else v) for k, v in full.items()}
+    d = to_device_batch(batch, dev)
+    w = torch.empty((B, 384), dtype=torch.float32, device=dev)
+    st = torch.empty((B,), dtype=torch.int32, device=dev)
+    it = torch.empty((B,), dtype=torch.int32, device=dev)
+    sync = lambda: torch.cuda.synchronize(dev)  # noqa: E731
+
+    # 8(f) row 1: the discrete dynamics built on the device -- its own HBM roofline, and the
+    # fused per-tick throughput build + solve
     if args.dynamics_steps > 0:
         N = 16
         dm = {k: torch.as_tensor(batch[k], dtype=torch.float32).contiguous().to(dev)
@@ -210,14 +517,14 @@ def main():
         for _ in range(2):
             plan.build_dynamics(dm["m"], dm["I_world"], dm["r_legs"], d["xref"], dt, out=outs,
                                 stream=stream)
-        torch.cuda.synchronize(dev)
+        sync()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(args.dynamics_steps):
             plan.build_dynamics(dm["m"], dm["I_world"], dm["r_legs"], d["xref"], dt, out=outs,
                                 stream=stream)
         e1.record(stream)
-        torch.cuda.synchronize(dev)
+        sync()
         dyn_ms = e0.elapsed_time(e1) / args.dynamics_steps
         dyn_bytes = B * (4 + 36 + N * 48 + N * 48 + 576 + N * 576 + 48)
         t0f = time.perf_counter()
@@ -226,63 +533,60 @@ def main():
                                 stream=stream)
             plan.solve(outs[0], outs[1], outs[2], d["x0"], d["xref"], d["contact"],
                        out=(w, st, it), stream=stream)
-        torch.cuda.synchronize(dev)
+        sync()
         fused = B * args.dynamics_steps / (time.perf_counter() - t0f)
         gbs = dyn_bytes / (dyn_ms * 1e-3) / 1e9
-        dyn = {"kernel": "dynamics_kernel", "ms_per_step": dyn_ms, "robots_per_s": B / (dyn_ms * 1e-3),
-               "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": gbs / HBM_PEAK_GBS, "bytes_per_robot": dyn_bytes // B},
-               "fused_build_and_solve_per_s": fused}
+        out["dynamics"] = {"kernel": "dynamics_kernel", "ms_per_step": dyn_ms,
+                           "robots_per_s": B / (dyn_ms * 1e-3),
+                           "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS,
+                                        "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+                                        "bytes_per_robot": dyn_bytes // B},
+                           "fused_build_and_solve_per_s": fused}
 
-    # warm start (centroidal_mpc.py:91-95).  Next-tick proxy: the state
-    # moves (x0 + noise), reference and gait stay; every warm step starts from the previous
-    # tick's (w, y).  Cold and warm solves of the same next-tick batch, same timing method.
-    warm = None
+    # 8(f) row 4: warm start (centroidal_mpc.py:91-95).  Next-tick proxy: the state moves
+    # (x0 + noise), reference and gait stay; every warm step starts from the previous tick's
+    # (w, y).  Cold and warm solves of the same next-tick batch, same timing method.
     if args.warm_steps > 0:
         y0 = torch.empty((B, 12 * 16), dtype=torch.float32, device=dev)
         plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"],
                    out=(w, st, it), stream=stream, y_out=y0)
         w0 = w.clone()
-        g = torch.Generator(device=dev).manual_seed(1234 + rank)
+        g = torch.Generator(device=dev).manual_seed(1234)
         sc = torch.tensor([2e-3] * 6 + [2e-2] * 6, device=dev)
         d2 = dict(d)
         d2["x0"] = (d["x0"] + torch.randn(d["x0"].shape, generator=g, device=dev) * sc).contiguous()
         y1 = torch.empty_like(y0)
 
         def timed(warm_on):
+            kw = dict(w_init=w0, y_init=y0, y_out=y1) if warm_on else {}
             for _ in range(2):
                 plan.solve(d2["Ad"], d2["Bd"], d2["gd"], d2["x0"], d2["xref"], d2["contact"],
-                           out=(w, st, it), stream=stream,
-                           **(dict(w_init=w0, y_init=y0, y_out=y1) if warm_on else {}))
-            torch.cuda.synchronize(dev)
+                           out=(w, st, it), stream=stream, **kw)
+            sync()
             ta = time.perf_counter()
             for _ in range(args.warm_steps):
                 plan.solve(d2["Ad"], d2["Bd"], d2["gd"], d2["x0"], d2["xref"], d2["contact"],
-                           out=(w, st, it), stream=stream,
-                           **(dict(w_init=w0, y_init=y0, y_out=y1) if warm_on else {}))
-            torch.cuda.synchronize(dev)
+                           out=(w, st, it), stream=stream, **kw)
+            sync()
             el = time.perf_counter() - ta
             itn = it.cpu().numpy()
             return (B * args.warm_steps / el, float(itn.mean()), (st == 1).float().mean().item(),
                     int(itn.max()), float(np.percentile(itn, 99.9)))
         cold_rate, cold_it, cold_ok, cold_max, cold_p = timed(False)
         warm_rate, warm_it, warm_ok, warm_max, warm_p = timed(True)
-        warm = {"scenario": "next tick: x0 + N(0, 2e-3 pos/rpy, 2e-2 vel/omega); warm from the "
-                            "previous tick's (w, y_out), cmpc_solve_warm",
-                "solves_per_s_warm": warm_rate, "solves_per_s_cold": cold_rate,
-                "speedup": warm_rate / cold_rate, "iters_mean_warm": warm_it,
-                "iters_mean_cold": cold_it, "solved_frac_warm": warm_ok,
-                "solved_frac_cold": cold_ok, "iters_max_warm": warm_max,
-                "iters_max_cold": cold_max, "iters_p999_warm": warm_p, "iters_p999_cold": cold_p}
+        out["warm_start"] = {
+            "scenario": "next tick: x0 + N(0, 2e-3 pos/rpy, 2e-2 vel/omega); warm from the "
+                        "previous tick's (w, y_out), cmpc_solve_warm",
+            "solves_per_s_warm": warm_rate, "solves_per_s_cold": cold_rate,
+            "speedup": warm_rate / cold_rate, "iters_mean_warm": warm_it,
+            "iters_mean_cold": cold_it, "solved_frac_warm": warm_ok,
+            "solved_frac_cold": cold_ok, "iters_max_warm": warm_max,
+            "iters_max_cold": cold_max, "iters_p999_warm": warm_p, "iters_p999_cold": cold_p}
 
-    # the whole tick on the device -- reference trajectory, contact table
-    # and foot levers (cmpc_generate_traj, com_trajectory.py:27-207) -> discrete dynamics -> solve.
-    # Inputs are what ComTraj.generate_traj reads from the robot (state, command, time, gait,
-    # current levers); the traj kernel gets its own HBM roofline.
-    tick = None
+    # 8(f) row 2: the whole tick on the device -- reference trajectory, contact table and foot
+    # levers (cmpc_generate_traj, com_trajectory.py:27-207) -> discrete dynamics -> solve.
     if args.tick_steps > 0:
-        tk = synth.make_tick_inputs(B, seed=synth.CONFIGS[min(cfg, 2)]["seed"] + 500 + 1000 * rank,
-                                    mixed=cfg != 1)
+        tk = synth.make_tick_inputs(B, seed=synth.CONFIGS[2]["seed"] + 500, mixed=True)
         f32, f64 = torch.float32, torch.float64
         td = {k: torch.as_tensor(tk[k], dtype=f64 if k in ("pos_des", "t_now", "gait") else f32)
               .contiguous().to(dev) for k in ("x0", "pos_des", "cmd", "t_now", "gait", "foot_lever",
@@ -307,38 +611,38 @@ def main():
                        out=(w, st, it), stream=stream)
         for _ in range(2):
             full_tick()
-        torch.cuda.synchronize(dev)
+        sync()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(args.tick_steps):
             gen()
         e1.record(stream)
-        torch.cuda.synchronize(dev)
+        sync()
         tr_ms = e0.elapsed_time(e1) / args.tick_steps
         tr_bytes = 48 + 24 + 16 + 8 + 48 + 48 + N * 48 + 4 * N + N * 48 + 24   # in + out per robot
         t0t = time.perf_counter()
         for _ in range(args.tick_steps):
             full_tick()
-        torch.cuda.synchronize(dev)
+        sync()
         tick_rate = B * args.tick_steps / (time.perf_counter() - t0t)
         td["pos_des"].copy_(pd0)
         tick_it = it.cpu().numpy()
         gbs_t = tr_bytes * B / (tr_ms * 1e-3) / 1e9
-        tick = {"kernel": "traj_group_kernel", "ms_per_step": tr_ms,
-                "roofline": {"bound": "hbm", "achieved": gbs_t, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": gbs_t / HBM_PEAK_GBS, "bytes_per_robot": tr_bytes},
-                "full_tick_per_s": tick_rate,
-                "full_tick": "generate_traj + build_dynamics + cold solve, all on the device",
-                "solved_frac": float((st == 1).float().mean().item()),
-                "iters_mean": float(tick_it.mean())}
+        out["tick"] = {"kernel": "traj_group_kernel", "ms_per_step": tr_ms,
+                       "roofline": {"bound": "hbm", "achieved": gbs_t, "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": gbs_t / HBM_PEAK_GBS,
+                                    "bytes_per_robot": tr_bytes},
+                       "full_tick_per_s": tick_rate,
+                       "full_tick": "generate_traj + build_dynamics + cold solve, all on the "
+                                    "device (mixed gaits)",
+                       "solved_frac": float((st == 1).float().mean().item()),
+                       "iters_mean": float(tick_it.mean())}
 
-    # the consumer of U[:, 0] -- the 1 kHz leg controller
-    # (leg_controller.py:43-112) for every robot of the batch, on the device, with synthetic
-    # Pinocchio quantities (random SPD M) and the solver's own forces.  HBM-bound.
-    leg = None
+    # 8(f) row 3: the consumer of U[:, 0] -- the 1 kHz leg controller (leg_controller.py:43-112)
+    # for every robot of the batch, with synthetic Pinocchio quantities and the solver's forces.
     if args.leg_steps > 0:
         from cmpc import leg_state
-        gl = torch.Generator(device=dev).manual_seed(77 + rank)
+        gl = torch.Generator(device=dev).manual_seed(77)
         f64 = torch.float64
         rn = lambda *sh, s=1.0: torch.randn(sh, generator=gl, device=dev, dtype=f64) * s  # noqa: E731
         Am = rn(B, 18, 18)
@@ -359,53 +663,52 @@ def main():
                             li["body"], li["hip"], stl, out=taul, stream=stream)
         for _ in range(2):
             leg_step()
-        torch.cuda.synchronize(dev)
+        sync()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(args.leg_steps):
             tl.add_(0.001)
             leg_step()
         e1.record(stream)
-        torch.cuda.synchronize(dev)
+        sync()
         leg_ms = e0.elapsed_time(e1) / args.leg_steps
-        # bytes the controller reads / writes per robot (fp64; C: the 12 leg-joint rows)
         leg_bytes = (8 + 48 + 48 + 288 + 1728 + 2592 + 1728 + 96 + 144 + 96 * 3 + 128 + 256
                      + 96 + 256)
         gbs_l = leg_bytes * B / (leg_ms * 1e-3) / 1e9
-        leg = {"kernel": "leg_kernel", "ms_per_step": leg_ms, "robots_per_s": B / (leg_ms * 1e-3),
-               "roofline": {"bound": "hbm", "achieved": gbs_l, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": gbs_l / HBM_PEAK_GBS, "bytes_per_robot": leg_bytes},
-               "note": "includes the small add_ on t per step; trot gait, 2 legs swing most ticks"}
+        out["leg_controller"] = {
+            "kernel": "leg_kernel", "ms_per_step": leg_ms, "robots_per_s": B / (leg_ms * 1e-3),
+            "roofline": {"bound": "hbm", "achieved": gbs_l, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs_l / HBM_PEAK_GBS, "bytes_per_robot": leg_bytes},
+            "note": "includes the small add_ on t per step; trot gait, 2 legs swing most ticks"}
         del li, Ml
 
     # BASELINE config 4 shape: robots in closed loop, every MPC tick on the device
-    # (generate_traj -> build_dynamics -> warm solve -> SRB plant for 20 leg ticks), recorded once
-    # as a HIP graph and replayed.  MuJoCo is absent: the plant is cmpc_srb_step's stand-in.
-    loop = None
+    # (generate_traj -> build_dynamics -> warm solve -> SRB plant for 20 leg ticks), recorded
+    # once as a HIP graph and replayed.  MuJoCo is absent: the plant is cmpc_srb_step's stand-in.
     if args.loop_steps > 0:
         from cmpc.closed_loop import ClosedLoop
         loop = {"plant": "cmpc_srb_step single-rigid-body stand-in (MuJoCo absent)",
                 "mpc_dt_s": 1 / 48}
         for nb in (1024, B):
-            cl = ClosedLoop(nb, plan=plan, seed=rank)
-            rg = np.random.default_rng(100 + rank)
+            cl = ClosedLoop(nb, plan=plan, seed=0)
+            rg = np.random.default_rng(100)
             cl.set_command(np.stack([rg.uniform(-0.5, 0.5, nb), rg.uniform(-0.2, 0.2, nb),
                                      np.full(nb, 0.27), rg.uniform(-1, 1, nb)], 1))
             for _ in range(4):
                 cl.tick()
-            torch.cuda.synchronize(dev)
+            sync()
             te = time.perf_counter()
             for _ in range(args.loop_steps):
                 cl.tick()
-            torch.cuda.synchronize(dev)
+            sync()
             eager = nb * args.loop_steps / (time.perf_counter() - te)
             cl.capture()
             cl.tick()
-            torch.cuda.synchronize(dev)
+            sync()
             tg = time.perf_counter()
             for _ in range(args.loop_steps):
                 cl.tick()
-            torch.cuda.synchronize(dev)
+            sync()
             el = time.perf_counter() - tg
             loop[f"robots_{nb}"] = {"robot_ticks_per_s_graph": nb * args.loop_steps / el,
                                     "ms_per_tick_graph": el / args.loop_steps * 1e3,
@@ -414,21 +717,20 @@ def main():
                                     "iters_mean": float(cl.iters.float().mean().item()),
                                     "com_z_min": float(cl.x[:, 2].min().item())}
             del cl
+        out["closed_loop"] = loop
 
     # BASELINE config 0: one robot through the reference's own API (CentroidalMPC.solve_QP, the
-    # drop-in of centroidal_mpc.py), warm-started every tick as the reference does; the reference
-    # budget per MPC tick is MPC_DT = 20.8 ms (test_MPC.py:67-68).
-    api = None
-    if args.api_ticks > 0 and rank == 0:
+    # drop-in of centroidal_mpc.py), warm-started every tick as the reference does; the
+    # reference budget per MPC tick is MPC_DT = 20.8 ms (test_MPC.py:67-68).
+    if args.api_ticks > 0:
+        import contextlib
         import types
-        sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
         from centroidal_mpc import CentroidalMPC
         one = synth.make_batch(1, seed=0)
         traj = types.SimpleNamespace(
             N=16, Ad=one["Ad"][0], Bd=one["Bd"][0], gd=one["gd"][0].reshape(12, 1),
             initial_x_vec=one["x0"][0].reshape(12, 1), contact_table=one["contact"][0].astype(np.int32),
             compute_x_ref_vec=lambda: one["xref"][0].T.copy())
-        import contextlib
         with contextlib.redirect_stdout(sys.stderr):  # the reference's init print (:225-230)
             mpc = CentroidalMPC(None, traj)
         st_ms, up_ms, wall = [], [], []
@@ -440,66 +742,16 @@ def main():
                 wall.append((time.perf_counter() - ta) * 1e3)
                 st_ms.append(mpc.solve_time)
                 up_ms.append(mpc.update_time)
-        api = {"path": "CentroidalMPC(go2, traj).solve_QP -> sol['x'].full(), 1 robot, warm",
-               "solve_time_ms": float(np.median(st_ms)), "update_time_ms": float(np.median(up_ms)),
-               "wall_ms_per_tick": float(np.median(wall)), "mpc_dt_budget_ms": 1e3 / 48,
-               "return_status": mpc.solver.stats()["return_status"]}
-
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(batch, args.cpu_seconds)
-
-    if rank == 0:
-        line = {
-            "metric": "batched QP solves/sec (N=16, 4-leg friction cone) at 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "solves/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": elapsed / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic",
-            "config": {"workload": f"cfg{cfg} Go2 QP batch (SURVEY.md 8(d)), "
-                                   f"{'trot 3Hz/0.6 fixed schedule' if cfg == 1 else 'mixed stance' if cfg == 2 else 'trot+mixed'}",
-                       "N": 16, "batch_per_gpu": B, "global_batch": B * world,
-                       "parallelism": f"instance-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
-                         "traffic": traffic,
-                         "kernel": f"solve_bin_kernel<{[96, 128, 160, 192][q]}>",
-                         "kernel_avg_ms": avg_ms, "solves_per_launch": n_in_bin,
-                         "bytes_per_solve": BYTES_PER_SOLVE},
-            "roofline_compute": {"bound": "mfma", "achieved": achieved_tfs,
-                                 "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
-                                 "frac": achieved_tfs / F32_MATRIX_PEAK_TFS,
-                                 "flops_per_solve": fl_bin / max(n_in_bin, 1)},
-            "cpu_baseline": cpu,
-            "solved_frac": solved_frac,
-            "iters_mean": float(np.mean(iters)),
-            "iters_max": int(np.max(iters)),
-            "latency_ms_b256": lat_ms,
-            "dynamics": dyn,
-            "warm_start": warm,
-            "tick": tick,
-            "leg_controller": leg,
-            "closed_loop": loop,
-            "config0_api": api,
-            "params_override": over or None,
-            "bin_ms_per_step": {str(c): round(float(ms_bins[i]) / args.steps, 4)
-                                for i, c in enumerate((96, 128, 160, 192))},
-            "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},
-        }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+        out["config0_api"] = {
+            "path": "CentroidalMPC(go2, traj).solve_QP -> sol['x'].full(), 1 robot, warm",
+            "solve_time_ms": float(np.median(st_ms)), "update_time_ms": float(np.median(up_ms)),
+            "wall_ms_per_tick": float(np.median(wall)), "mpc_dt_budget_ms": 1e3 / 48,
+            "return_status": mpc.solver.stats()["return_status"]}
+    return out
 
 
 def cpu_baseline(batch, seconds):
-    """Time oracle/osqp_ref (C restatement of the reference's OSQP solve) on host cores."""
+    """Time oracle/osqp_ref (C++ restatement of the reference's OSQP solve) on host cores."""
     try:
         sys.path.insert(0, str(REPO))
         from oracle import osqp_ref

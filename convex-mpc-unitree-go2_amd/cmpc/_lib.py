@@ -43,6 +43,10 @@ EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_d
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_last_error", "cmpc_version")
 NUM_BINS = 4
 BIN_CAPS = (96, 128, 160, 192)
+# solve kernels (register classes): 0 = bins NC 128 + 96, 1 = bins NC 192 + 160
+NUM_SOLVE_KERNELS = 2
+KERNEL_BINS = ((1, 0), (3, 2))
+KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<192, 160>")
 
 _lib = None
 

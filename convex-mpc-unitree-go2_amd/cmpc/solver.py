@@ -86,8 +86,11 @@ class Plan:
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise CmpcError("cmpc: no ROCm device available (the solver has no CPU fallback)")
-        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
-                                   else torch.device(device).index or 0)
+        dv = torch.device("cuda") if device is None else torch.device(device)
+        if dv.type != "cuda":
+            raise ValueError(f"cmpc: plan device must be a ROCm (cuda) device, got {dv}")
+        self.device = torch.device("cuda", torch.cuda.current_device() if dv.index is None
+                                   else dv.index)
         with torch.cuda.device(self.device):
             h = ctypes.c_void_p()
             cp = self.params.to_c()
@@ -106,17 +109,25 @@ class Plan:
         except Exception:
             pass
 
+    def _same_device(self, t: torch.Tensor):
+        """The plan's workspace and streams live on self.device: every tensor must too."""
+        if t.device != self.device:
+            raise ValueError(f"cmpc: tensors are on {t.device} but the plan was created on "
+                             f"{self.device}")
+
     def set_timing(self, enable: bool):
         _check(self.lib, self.lib.cmpc_plan_set_timing(self._h, int(bool(enable))),
                "cmpc_plan_set_timing")
 
     def timing_read(self):
-        """-> (ms_per_bin[4], calls_per_bin[4]) of the solve kernels since the last read."""
-        ms = (ctypes.c_float * _lib.NUM_BINS)()
-        calls = (ctypes.c_int32 * _lib.NUM_BINS)()
+        """-> (ms_per_kernel[2], calls_per_kernel[2]) of the two solve kernels since the last
+        read (kernel 0: bins NC 128 + 96; kernel 1: bins NC 192 + 160, _lib.KERNEL_BINS)."""
+        ms = (ctypes.c_float * 4)()       # room for the round-1 ABI's four slots (A/B builds)
+        calls = (ctypes.c_int32 * 4)()
         _check(self.lib, self.lib.cmpc_plan_timing_read(self._h, ms, calls),
                "cmpc_plan_timing_read")
-        return list(ms), list(calls)
+        k = _lib.NUM_SOLVE_KERNELS
+        return list(ms)[:k], list(calls)[:k]
 
     def solve(self, Ad, Bd, gd, x0, xref, contact, out=None, stream=None, w_init=None,
               y_init=None, y_out=None):
@@ -138,6 +149,7 @@ class Plan:
         _dev_tensor(x0, "x0", f32, (B, 12))
         _dev_tensor(xref, "xref", f32, (B, N, 12))
         _dev_tensor(contact, "contact", torch.uint8, (B, 4, N))
+        self._same_device(Ad)
         for t in (Bd, gd, x0, xref, contact):
             if t.device != Ad.device:
                 raise ValueError("all inputs must be on the same device")
@@ -194,6 +206,7 @@ class Plan:
         _dev_tensor(inertia, "inertia", f32, (B, 3, 3))
         _dev_tensor(r_feet, "r_feet", f32, (B, N, 4, 3))
         _dev_tensor(xref, "xref", f32, (B, N, 12))
+        self._same_device(mass)
         for t in (inertia, r_feet, xref):
             if t.device != mass.device:
                 raise ValueError("all inputs must be on the same device")
@@ -237,6 +250,7 @@ class Plan:
         _dev_tensor(gait, "gait", f64, (B, 6))
         _dev_tensor(foot_lever, "foot_lever", f32, (B, 4, 3))
         _dev_tensor(hip, "hip", f32, (4, 3))
+        self._same_device(x0)
         for t in (pos_des, cmd, t_now, gait, foot_lever, hip):
             if t.device != x0.device:
                 raise ValueError("all inputs must be on the same device")
@@ -284,6 +298,9 @@ class Plan:
                              ("body", body, (B, 16)), ("hip", hip, (4, 3)),
                              ("state", state, (B, 4, 8))):
             _dev_tensor(x, name, f64, shp)
+        for x in (t, gait, force, J_foot, J_full, M, C, g, dq, Jdot_dq, foot_pos, foot_vel, body,
+                  hip, state):
+            self._same_device(x)
         tau = torch.empty((B, 12), dtype=f64, device=t.device) if out is None else out
         _dev_tensor(tau, "tau", f64, (B, 12))
         if stream is None:

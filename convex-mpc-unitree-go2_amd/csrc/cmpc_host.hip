@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 #include <string>
 #include <vector>
@@ -18,6 +19,8 @@
 #include "cmpc_leg.hip"       // leg controller (stance torque mapping, swing) kernel
 #include "cmpc_sim.hip"       // single-rigid-body plant (closed-loop stand-in for MuJoCo)
 
+constexpr int kNumGroups = 2;  // solve kernels (register classes), see solve_group_kernel
+
 struct cmpc_plan {
   cmpc_params p;
   cmpc::KParams kp;
@@ -25,18 +28,20 @@ struct cmpc_plan {
   int cus = 0;      // compute units of the device
   int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
-  float* d_work;    // per-wave park slabs; bin q's region starts at work_off[q] (bins run concurrently)
-  size_t work_off[cmpc::kNumBins];
-  int grid[cmpc::kNumBins];
-  int threads[cmpc::kNumBins];
-  // per-bin streams: the bins' persistent kernels run concurrently so one bin's tail (its last
-  // long-running instances) overlaps the other bins' work; forked from / joined to the caller
-  hipStream_t bin_stream[cmpc::kNumBins] = {};
+  float* d_work;    // per-wave park slabs; group k's region starts at work_off[k] (groups overlap)
+  size_t work_off[kNumGroups];
+  size_t slab[kNumGroups];
+  int grid[kNumGroups];
+  // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
+  // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
+  // stream forked from / joined to it.  Two streams in total stay within the device's hardware
+  // queues (GPU_MAX_HW_QUEUES = 4), so the classes overlap instead of sharing a queue.
+  hipStream_t side = nullptr;
   hipEvent_t fork = nullptr;
-  hipEvent_t join[cmpc::kNumBins] = {};
+  hipEvent_t join = nullptr;
   // timing hooks
   bool timing = false;
-  struct Rec { hipEvent_t a, b; int bin; };
+  struct Rec { hipEvent_t a, b; int group; };
   std::vector<Rec> recs;       // recorded (pending) pairs
   std::vector<Rec> pool;       // free event pairs
 };
@@ -54,33 +59,30 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 using KernelFn = void (*)(cmpc::KParams, cmpc::Inputs, cmpc::Outputs, const int*, const int*,
-                          int*, float*);
+                          const int*, int*, int, float*, size_t);
 
-int bin_threads(int q) {
-  switch (q) {
-    case 0: return cmpc::Cfg<96>::THREADS;
-    case 1: return cmpc::Cfg<128>::THREADS;
-    case 2: return cmpc::Cfg<160>::THREADS;
-    default: return cmpc::Cfg<192>::THREADS;
-  }
+// The plan's workspace, streams and events belong to the device current at cmpc_plan_create:
+// every launch must run there (the Python layer makes the tensors' device current).
+int check_device(const cmpc_plan* pl, const char* what) {
+  int dev = -1;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+  if (dev != pl->device)
+    return fail(CMPC_E_INVALID, std::string(what) + ": the current device is not the plan's device");
+  return CMPC_OK;
 }
 
-size_t bin_slab(int q) {
-  switch (q) {
-    case 0: return cmpc::Cfg<96>::SLAB;
-    case 1: return cmpc::Cfg<128>::SLAB;
-    case 2: return cmpc::Cfg<160>::SLAB;
-    default: return cmpc::Cfg<192>::SLAB;
-  }
+// group 0: bins 1 (NC 128) then 0 (NC 96), two waves per SIMD; group 1: bins 3 (NC 192) then
+// 2 (NC 160), one wave per SIMD.  qa = the group's first (larger) bin.
+int group_first_bin(int k) { return k == 0 ? 1 : 3; }
+
+size_t group_slab(int k) {
+  return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
+                : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
 }
 
-KernelFn bin_fn(int q) {
-  switch (q) {
-    case 0: return cmpc::solve_bin_kernel<96>;
-    case 1: return cmpc::solve_bin_kernel<128>;
-    case 2: return cmpc::solve_bin_kernel<160>;
-    default: return cmpc::solve_bin_kernel<192>;
-  }
+KernelFn group_fn(int k) {
+  return k == 0 ? cmpc::solve_group_kernel<128, 96> : cmpc::solve_group_kernel<192, 160>;
 }
 }  // namespace
 
@@ -164,10 +166,9 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   pl->cus = cus;
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
   size_t work_floats = 0;
-  for (int q = 0; q < cmpc::kNumBins; ++q) {
+  for (int k = 0; k < kNumGroups; ++k) {
     int nb = 0;
-    pl->threads[q] = bin_threads(q);
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, bin_fn(q), pl->threads[q], 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64, 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
 #ifdef CMPC_STAMPS
@@ -176,9 +177,10 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
       if (c >= 1 && c < nb) nb = c;
     }
 #endif
-    pl->grid[q] = nb * cus;
-    pl->work_off[q] = work_floats;
-    work_floats += (size_t)pl->grid[q] * bin_slab(q);
+    pl->grid[k] = nb * cus;
+    pl->slab[k] = group_slab(k);
+    pl->work_off[k] = work_floats;
+    work_floats += (size_t)pl->grid[k] * pl->slab[k];
   }
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
@@ -195,16 +197,11 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
-  for (int q = 0; q < cmpc::kNumBins; ++q) {
-    if ((e = hipStreamCreateWithFlags(&pl->bin_stream[q], hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&pl->join[q], hipEventDisableTiming)) != hipSuccess) {
-      cmpc_plan_destroy(pl);
-      return hip_fail(e, "bin stream/event creation");
-    }
-  }
-  if ((e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess) {
+  if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&pl->join, hipEventDisableTiming)) != hipSuccess) {
     cmpc_plan_destroy(pl);
-    return hip_fail(e, "hipEventCreateWithFlags");
+    return hip_fail(e, "side stream/event creation");
   }
   *out = pl;
   g_err.clear();
@@ -241,8 +238,41 @@ int cmpc_solve_warm(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd,
                     cmpc::Outputs{w_out, status, iters, y_out}, stream);
 }
 
+static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParams& kp,
+                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
+  hipError_t e;
+  cmpc_plan::Rec rec{nullptr, nullptr, k};
+  const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
+  if (rec_this) {
+    if (!pl->pool.empty()) {
+      rec = pl->pool.back();
+      pl->pool.pop_back();
+      rec.group = k;
+    } else {
+      if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+      if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    }
+    if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  const int qa = group_first_bin(k);
+  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64), 0, s, kp, in, out,
+                     pl->d_lists + (size_t)qa * pl->p.max_batch,
+                     pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
+                     pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
+                     pl->slab[k]);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "solve_group_kernel launch");
+  if (rec_this) {
+    if ((e = hipEventRecord(rec.b, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    pl->recs.push_back(rec);
+  }
+  return CMPC_OK;
+}
+
 static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cmpc::Outputs& out,
                       void* stream) {
+  int rc = check_device(pl, "cmpc_solve");
+  if (rc != CMPC_OK) return rc;
   hipStream_t st = (hipStream_t)stream;
   hipError_t e = hipMemsetAsync(pl->d_counters, 0, 2 * cmpc::kNumBins * sizeof(int), st);
   if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
@@ -252,50 +282,26 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
                      in.contact, pl->d_counters, pl->d_lists, pl->p.max_batch);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
-  if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-  int launched[cmpc::kNumBins] = {0};
-  // largest bin first: its persistent waves (one per SIMD at NC >= 160) take the CUs first and
-  // the cheaper bins fill in behind them, so the batch does not end on a late-started big bin
-  // (cfg2 +2-3 %)
-  for (int qi = 0; qi < cmpc::kNumBins; ++qi) {
-    const int q = cmpc::kNumBins - 1 - qi;
-    if (q > 0 && cmpc::kBinCap[q - 1] >= 12 * pl->kp.N) continue;  // bins beyond 12N are empty
-    const long long g = pl->grid[q] < B ? pl->grid[q] : B;
-    hipStream_t bs = pl->bin_stream[q];
-    if ((e = hipStreamWaitEvent(bs, pl->fork, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-    cmpc_plan::Rec rec{nullptr, nullptr, q};
-    const bool rec_this = pl->timing && pl->recs.size() < 4096 * cmpc::kNumBins;
-    if (rec_this) {
-      if (!pl->pool.empty()) {
-        rec = pl->pool.back();
-        pl->pool.pop_back();
-        rec.bin = q;
-      } else {
-        if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-        if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-      }
-      if ((e = hipEventRecord(rec.a, bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    }
-    cmpc::KParams kp = pl->kp;
-    // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
-    kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
-    hipLaunchKernelGGL(bin_fn(q), dim3((unsigned)g), dim3(pl->threads[q]), 0, bs, kp, in,
-                       out, pl->d_lists + (size_t)q * pl->p.max_batch, pl->d_counters + q,
-                       pl->d_counters + cmpc::kNumBins + q, pl->d_work + pl->work_off[q]);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "solve_bin_kernel launch");
-    if (rec_this) {
-      if ((e = hipEventRecord(rec.b, bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-      pl->recs.push_back(rec);
-    }
-    if ((e = hipEventRecord(pl->join[q], bs)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    launched[q] = 1;
-  }
-  for (int q = 0; q < cmpc::kNumBins; ++q) {
-    if (!launched[q]) continue;
-    if ((e = hipStreamWaitEvent(st, pl->join[q], 0)) != hipSuccess)
+  cmpc::KParams kp = pl->kp;
+  // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
+  kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
+  // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
+  // fills them); it exists only when a step can hold more than 128 / 12 stance legs
+  const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
+  if (big) {
+    if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
+    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+    rc = record_launch(pl, 1, pl->side, kp, in, out, g1);
+    if (rc != CMPC_OK) return rc;
+    if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
+  const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
+  rc = record_launch(pl, 0, st, kp, in, out, g0);
+  if (rc != CMPC_OK) return rc;
+  if (big && (e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
+    return hip_fail(e, "hipStreamWaitEvent");
   return CMPC_OK;
 }
 
@@ -303,6 +309,7 @@ int cmpc_build_dynamics(cmpc_plan* pl, int64_t B, float dt, const float* mass,
                         const float* inertia, const float* r_feet, const float* xref, float* Ad,
                         float* Bd, float* gd, void* stream) {
   if (!pl) return fail(CMPC_E_INVALID, "cmpc_build_dynamics: null plan");
+  if (int rc = check_device(pl, "cmpc_build_dynamics")) return rc;
   if (B < 0) return fail(CMPC_E_INVALID, "cmpc_build_dynamics: negative batch");
   if (!(dt > 0.f) || !std::isfinite(dt)) return fail(CMPC_E_INVALID, "cmpc_build_dynamics: dt must be > 0");
   if (B == 0) return CMPC_OK;
@@ -326,6 +333,7 @@ int cmpc_generate_traj(cmpc_plan* pl, int64_t B, double dt, const float* x0, dou
                        const float* foot_lever, const float* hip, float* xref, uint8_t* contact,
                        float* r_feet, void* stream) {
   if (!pl) return fail(CMPC_E_INVALID, "cmpc_generate_traj: null plan");
+  if (int rc = check_device(pl, "cmpc_generate_traj")) return rc;
   if (B < 0) return fail(CMPC_E_INVALID, "cmpc_generate_traj: negative batch");
   if (!(dt > 0.0) || !std::isfinite(dt)) return fail(CMPC_E_INVALID, "cmpc_generate_traj: dt must be > 0");
   if (B == 0) return CMPC_OK;
@@ -354,6 +362,7 @@ int cmpc_leg_torque(cmpc_plan* pl, int64_t B, const double* t, const double* gai
                     const double* foot_vel, const double* body, const double* hip,
                     double* state, double tau_max, double* tau, void* stream) {
   if (!pl) return fail(CMPC_E_INVALID, "cmpc_leg_torque: null plan");
+  if (int rc = check_device(pl, "cmpc_leg_torque")) return rc;
   if (B < 0) return fail(CMPC_E_INVALID, "cmpc_leg_torque: negative batch");
   if (force_stride < 12) return fail(CMPC_E_INVALID, "cmpc_leg_torque: force_stride must be >= 12");
   if (!std::isfinite(tau_max)) return fail(CMPC_E_INVALID, "cmpc_leg_torque: tau_max must be finite");
@@ -376,6 +385,7 @@ int cmpc_srb_step(cmpc_plan* pl, int64_t B, int nsub, double dt, const double* t
                   const float* force, int64_t force_stride, const float* hip, float* x,
                   float* feet, uint8_t* contact_state, void* stream) {
   if (!pl) return fail(CMPC_E_INVALID, "cmpc_srb_step: null plan");
+  if (int rc = check_device(pl, "cmpc_srb_step")) return rc;
   if (B < 0 || nsub < 0) return fail(CMPC_E_INVALID, "cmpc_srb_step: negative batch or nsub");
   if (!(dt > 0.0) || !std::isfinite(dt)) return fail(CMPC_E_INVALID, "cmpc_srb_step: dt must be > 0");
   if (force_stride < 12) return fail(CMPC_E_INVALID, "cmpc_srb_step: force_stride must be >= 12");
@@ -397,18 +407,18 @@ int cmpc_plan_set_timing(cmpc_plan* pl, int enable) {
   return CMPC_OK;
 }
 
-int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_bin, int32_t* calls_per_bin) {
-  if (!pl || !ms_per_bin || !calls_per_bin)
+int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_kernel, int32_t* calls_per_kernel) {
+  if (!pl || !ms_per_kernel || !calls_per_kernel)
     return fail(CMPC_E_INVALID, "cmpc_plan_timing_read: null argument");
-  for (int q = 0; q < cmpc::kNumBins; ++q) { ms_per_bin[q] = 0.f; calls_per_bin[q] = 0; }
+  for (int k = 0; k < kNumGroups; ++k) { ms_per_kernel[k] = 0.f; calls_per_kernel[k] = 0; }
   for (auto& r : pl->recs) {
     hipError_t e = hipEventSynchronize(r.b);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
     float ms = 0.f;
     e = hipEventElapsedTime(&ms, r.a, r.b);
     if (e != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
-    ms_per_bin[r.bin] += ms;
-    calls_per_bin[r.bin] += 1;
+    ms_per_kernel[r.group] += ms;
+    calls_per_kernel[r.group] += 1;
     pl->pool.push_back(r);
   }
   pl->recs.clear();
@@ -419,11 +429,9 @@ void cmpc_plan_destroy(cmpc_plan* pl) {
   if (!pl) return;
   for (auto& r : pl->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto& r : pl->pool) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
-  for (int q = 0; q < cmpc::kNumBins; ++q) {
-    if (pl->bin_stream[q]) (void)hipStreamDestroy(pl->bin_stream[q]);
-    if (pl->join[q]) (void)hipEventDestroy(pl->join[q]);
-  }
+  if (pl->side) (void)hipStreamDestroy(pl->side);
   if (pl->fork) (void)hipEventDestroy(pl->fork);
+  if (pl->join) (void)hipEventDestroy(pl->join);
   (void)hipFree(pl->d_counters);
   (void)hipFree(pl->d_lists);
   (void)hipFree(pl->d_work);

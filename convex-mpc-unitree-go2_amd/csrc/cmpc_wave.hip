@@ -1328,6 +1328,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   }
   build_admm_basis<NC>(s, P, Bg, ntri);
   const int n = 3 * ntri;
+  // initial rho per bin: the NC = 128 bin (33-42 stance triples, trot-like schedules) converges
+  // in fewer iterations from rho0 / 2; its hard instances (a failed polish session) go back to
+  // rho0, where they converge as before (cfg1 +6-10 %, cfg2 +1 %; rho0 / 2 for every bin loses
+  // 7 % on cfg2, DESIGN.md 7)
+  float rho = (NC == 128) ? 0.5f * P.rho0 : P.rho0;
+  bool rho_low = NC == 128;  // still at the bin's reduced initial rho
   s.pcode[lane] = -1;
   if (in.w_init == nullptr && in.y_init == nullptr) {
     for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; s.y[p] = 0.f; }
@@ -1356,8 +1362,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     float pv[3], qv[3];
     project(u[0], u[1], u[2], P.mu, P.fz_min, pv[0], pv[1], pv[2]);
     int code;
-    if (in.y_init) {  // the dual pushes the faces it holds outward
-      const float ir = 1.f / P.rho0;
+    if (in.y_init) {  // the dual pushes the faces it holds outward (at the bin's initial rho)
+      const float ir = 1.f / rho;
       code = project(pv[0] + yv[0] * ir, pv[1] + yv[1] * ir, pv[2] + yv[2] * ir, P.mu, P.fz_min,
                      qv[0], qv[1], qv[2]);
     } else {          // primal only: the faces the warm point lies on, to fp32 rounding
@@ -1384,12 +1390,6 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
 #endif
   bool polished = false;
-  // initial rho per bin: the NC = 128 bin (33-42 stance triples, trot-like schedules) converges
-  // in fewer iterations from rho0 / 2; its hard instances (a failed polish session) go back to
-  // rho0, where they converge as before (cfg1 +6-10 %, cfg2 +1 %; rho0 / 2 for every bin loses
-  // 7 % on cfg2, DESIGN.md 7)
-  float rho = (NC == 128) ? 0.5f * P.rho0 : P.rho0;
-  bool rho_low = NC == 128;  // still at the bin's reduced initial rho
   float rp = 0.f, rd = 0.f, np_ = 0.f, nd = 0.f;
   int stable = 0;
   bool refactor = n > 0;  // (re)build + invert the matrix for the current basis
@@ -1611,7 +1611,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #endif
       CMPC_T0(t_ps);
 #ifndef CMPC_NO_PARK
-      parked = !refactor;  // a pending refactor (rho changed) makes the current inverse stale
+      // a pending refactor (rho changed) makes the current inverse stale, and a first session
+      // at the bin's reduced rho refactors at rho0 when it fails: nothing to park for either
+      parked = !refactor && !rho_low;
       if (parked) park_store<NC>(park, M);  // restored if the polish fails
 #else
       parked = false;      // a failed polish refactors the ADMM matrix instead
@@ -1675,23 +1677,19 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   CMPC_ACC(5, t_inst);
 }
 
+// Drain one bin's queue with this wave (persistent: instance ids come from a device counter).
 template <int NC>
-__global__ void __launch_bounds__(64, Cfg<NC>::WPE)
-    solve_bin_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list,
-                     const int* __restrict__ count, int* __restrict__ head,
-                     float* __restrict__ work) {
-  using C = Cfg<NC>;
-  __shared__ Smem<NC> s;
+__device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const Inputs& in,
+                                          const Outputs& out, const int* __restrict__ list,
+                                          const int* __restrict__ count, int* __restrict__ head,
+                                          float* __restrict__ park) {
   const int lane = opaque_lane();
-  float* park = work + (size_t)blockIdx.x * C::SLAB;
-  if (lane < 12) {
+  WSYNC();
+  if (lane < 12) {  // KParams copies (each bin's Smem layout places them differently)
     s.Q2[lane] = P.Q2[lane];
     s.R2[lane] = P.R2[lane];
   }
   const int total = *count;
-#ifdef CMPC_STAMPS
-  if (lane < 16) s.st[lane] = 0;
-#endif
   for (;;) {
     int idx = 0;
     if (lane == 0) idx = atomicAdd(head, 1);
@@ -1699,9 +1697,36 @@ __global__ void __launch_bounds__(64, Cfg<NC>::WPE)
     if (idx >= total) break;
     solve_instance<NC>(s, P, (int64_t)list[idx], in, out, park);
   }
+}
+
+// One persistent kernel per register class: bins NCA and NCB share the occupancy (two waves per
+// SIMD for NC <= 128, one for NC >= 160), so one kernel serves both, draining the larger bin
+// first (its instances are the slower ones: hardest first shortens the batch tail).  Two
+// kernels instead of four keep the solve within the device's hardware queues (the caller's
+// stream + one plan stream), so the two classes really overlap.
+template <int NCA, int NCB>
+__global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
+    solve_group_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
+                       const int* __restrict__ list_b, const int* __restrict__ counts,
+                       int* __restrict__ heads, int qa, float* __restrict__ work,
+                       size_t slab) {
+  static_assert(Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
+  constexpr size_t kBytes = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
+                                                                   : sizeof(Smem<NCB>);
+  __shared__ __attribute__((aligned(16))) unsigned char raw[kBytes];
+  float* park = work + (size_t)blockIdx.x * slab;
+#ifdef CMPC_STAMPS
+  // st[] is the first member of every Smem<NC>: one set of totals for the wave
+  Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(raw);
+  if (threadIdx.x < 16) s0.st[threadIdx.x] = 0;
+#endif
+  drain_bin<NCA>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa, heads + qa,
+                 park);
+  drain_bin<NCB>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
+                 heads + qa - 1, park);
 #ifdef CMPC_STAMPS
   WSYNC();
-  if (lane < 16) atomicAdd(&g_stamps[lane], s.st[lane]);
+  if (threadIdx.x < 16) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
 #endif
 }
 

@@ -85,7 +85,8 @@ typedef struct cmpc_plan cmpc_plan;
 /* Fill *p with defaults.  Replaces the OPTS dict (centroidal_mpc.py:20-36). */
 void cmpc_params_default(cmpc_params* p);
 
-/* Validate params, allocate workspace for max_batch instances on the current device.
+/* Validate params, allocate workspace for max_batch instances on the current device.  Every
+ * later call with this plan must run with that device current (else CMPC_E_INVALID).
  * Replaces CentroidalMPC.__init__/_build_sparse_matrix (centroidal_mpc.py:41-67,178-230). */
 int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out);
 
@@ -205,13 +206,17 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
                   const float* force, int64_t force_stride, const float* hip, float* x,
                   float* feet, uint8_t* contact_state, void* stream);
 
-/* Measurement hooks (not on the reference's interface; used by bench.py).  While enabled,
- * cmpc_solve records a hipEvent pair around every solve-kernel launch (one per free-variable
- * bin; the bins run concurrently on plan-internal streams joined back to `stream`).  cmpc_plan_timing_read waits for the recorded events, returns the
- * summed kernel milliseconds per bin (ms_per_bin[4]) and launch counts (calls_per_bin[4]) since
- * the last read, and resets them.  At most 4096 solve calls are recorded between reads. */
+/* Measurement hooks (not on the reference's interface; used by bench.py).  A solve runs two
+ * persistent kernels, one per register class: kernel 0 serves the free-variable bins NC 128 and
+ * 96 on `stream`, kernel 1 the bins NC 192 and 160 on one plan-internal stream forked from and
+ * joined back to `stream` (the two overlap).  While enabled, cmpc_solve records a hipEvent pair
+ * around each kernel launch on its own stream; cmpc_plan_timing_read waits for the recorded
+ * events, returns the summed milliseconds per kernel (ms_per_kernel[CMPC_NUM_SOLVE_KERNELS]) and
+ * launch counts since the last read, and resets them.  At most 4096 solve calls are recorded
+ * between reads. */
+#define CMPC_NUM_SOLVE_KERNELS 2
 int cmpc_plan_set_timing(cmpc_plan* plan, int enable);
-int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_bin, int32_t* calls_per_bin);
+int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_kernel, int32_t* calls_per_kernel);
 
 /* Thread-local description of the last error returned on this thread ("" if none). */
 const char* cmpc_last_error(void);

@@ -366,6 +366,74 @@ def make_hard_fixture(name: str = "qp_hard.npz"):
     print(name, len(W), "instances, max KKT residual", np.max(KKT))
 
 
+def import_reference_mpc():
+    """Import centroidal_mpc.py from the reference with ``casadi`` replaced by the
+    conversion-only stand-in (tests/golden/casadi_standin.py; CasADi is not installed) and the
+    Pinocchio robot module by the synthetic stand-in, so the reference's QP assembly runs
+    unmodified."""
+    import_reference()
+    sys.path.insert(0, str(HERE))
+    import casadi_standin
+    sys.modules["casadi"] = casadi_standin
+    import centroidal_mpc  # noqa: F401
+    return centroidal_mpc
+
+
+def _traj_standin(Ad, Bd, gd, x0, xref, contact):
+    """The ComTraj fields CentroidalMPC reads (centroidal_mpc.py:46, 59-67, 122-285)."""
+    N = Bd.shape[0]
+    return types.SimpleNamespace(
+        N=N, Ad=np.array(Ad, dtype=np.float64), Bd=np.array(Bd, dtype=np.float64),
+        gd=np.array(gd, dtype=np.float64).reshape(12, 1),
+        initial_x_vec=np.array(x0, dtype=np.float64).reshape(12, 1),
+        contact_table=np.array(contact, dtype=np.int32),
+        compute_x_ref_vec=lambda: np.array(xref, dtype=np.float64).T.copy())
+
+
+def make_qp_assembly(name: str = "qp_assembly.npz", n_with_A: int = 16):
+    """Golden vectors of the reference's own QP assembly (centroidal_mpc.py:41-67, 122-359) for
+    every instance of the qp_cfg1 / qp_cfg2 / qp_hard fixtures, by CentroidalMPC itself:
+    ``__init__`` (incl. the structure print of _build_sparse_matrix), then per instance
+    ``_update_sparse_matrix`` -> (g, A, lba, uba) and ``_compute_bounds`` -> (lbx, ubx).  A is
+    kept (values on its structural pattern, CSC) for the first `n_with_A` instances."""
+    import contextlib
+    import io
+    cm = import_reference_mpc()
+    rows = {k: [] for k in ("g", "lba", "uba", "lbx", "ubx", "src")}
+    A_vals = []
+    pattern = None
+    H = None
+    printed = None
+    k = 0
+    for fname in ("qp_cfg1.npz", "qp_cfg2.npz", "qp_hard.npz"):
+        fx = np.load(HERE / fname)
+        for i in range(fx["w"].shape[0]):
+            traj = _traj_standin(fx["Ad"][i], fx["Bd"][i], fx["gd"][i], fx["x0"][i],
+                                 fx["xref"][i], fx["contact"][i])
+            if printed is None:
+                buf = io.StringIO()
+                with contextlib.redirect_stdout(buf):
+                    mpc = cm.CentroidalMPC(None, traj)
+                printed = buf.getvalue()
+                H = mpc.H_const.full()
+            g, A, lb, ub = mpc._update_sparse_matrix(traj)
+            lbx, ubx = mpc._compute_bounds(traj)
+            if pattern is None:
+                pattern = A.sparsity()
+            assert np.array_equal(A.sparsity().mask, pattern.mask)
+            if k < n_with_A:
+                A_vals.append(np.array(A.nonzeros()))
+            for key, v in (("g", g), ("lba", lb), ("uba", ub), ("lbx", lbx), ("ubx", ubx)):
+                rows[key].append(v.full().reshape(-1))
+            rows["src"].append([("qp_cfg1.npz", "qp_cfg2.npz", "qp_hard.npz").index(fname), i])
+            k += 1
+    colind, row = pattern.csc()
+    np.savez_compressed(HERE / name, H=H, A_colind=colind, A_row=row, A_vals=np.array(A_vals),
+                        A_shape=np.array(pattern.size()), init_print=np.array(printed),
+                        **{key: np.array(v) for key, v in rows.items()})
+    print(name, k, "instances;", printed.strip().splitlines()[1:3])
+
+
 if __name__ == "__main__":
     make_ref_inputs()
     make_traj_ticks()
@@ -373,3 +441,4 @@ if __name__ == "__main__":
     make_qp_fixture(1, 32, "qp_cfg1.npz")
     make_qp_fixture(2, 64, "qp_cfg2.npz")
     make_hard_fixture()
+    make_qp_assembly()

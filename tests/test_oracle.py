@@ -1,10 +1,13 @@
 """CPU: the oracle (oracle/) against the reference's own outputs and invariants.
 
-ref_inputs.npz was produced by running the reference's gait.py / com_trajectory.py
-(tests/golden/make_golden.py); the QP fixtures hold KKT-certified optima.
+ref_inputs.npz was produced by running the reference's gait.py / com_trajectory.py;
+qp_assembly.npz by running the reference's CentroidalMPC QP assembly (centroidal_mpc.py:41-67,
+122-359) unmodified under a conversion-only casadi stand-in (tests/golden/make_golden.py,
+tests/golden/casadi_standin.py); the QP fixtures hold KKT-certified optima.
 """
 import numpy as np
 import pytest
+import scipy.sparse as sp
 
 from oracle import mpc_qp, tight_solver
 from cmpc import synth
@@ -101,3 +104,78 @@ def test_duals_recovered_from_primal():
         scale = max(1e-3, np.max(np.abs(fx["lam_a"][i])))
         assert np.max(np.abs(la - fx["lam_a"][i])) < 1e-6 * scale + 1e-9
         assert np.max(np.abs(lx - fx["lam_x"][i])) < 1e-6 * scale + 1e-9
+
+
+# ---- the QP assembly against the reference's own CentroidalMPC (qp_assembly.npz) ----------
+def _assembly():
+    return load_fixture("qp_assembly.npz")
+
+
+def _ref_A(asm, j):
+    shape = tuple(int(x) for x in asm["A_shape"])
+    return sp.csc_matrix((asm["A_vals"][j], asm["A_row"], asm["A_colind"]), shape=shape)
+
+
+def _fixture_instance(src):
+    names = ("qp_cfg1.npz", "qp_cfg2.npz", "qp_hard.npz")
+    fx = load_fixture(names[int(src[0])])
+    return fx, int(src[1])
+
+
+def test_reference_init_print_structure():
+    """The reference's own __init__ / _build_sparse_matrix print (centroidal_mpc.py:225-230),
+    captured when make_golden ran it: H 384 x 384 nnz 384, A 448 x 384 nnz 5168."""
+    txt = str(_assembly()["init_print"])
+    assert "H:  384 x 384  | nnz =    384" in txt
+    assert "A:  448 x 384  | nnz =   5168 | dens =  0.0300" in txt
+    assert "constr: 448 | horizon N = 16" in txt
+
+
+def test_qp_assembly_vectors_match_reference_run():
+    """g, lba, uba (_update_sparse_matrix, :235-285) and lbx, ubx (_compute_bounds, :122-176)
+    from the reference's own code equal oracle.mpc_qp.build_qp on all 100 fixture instances."""
+    asm = _assembly()
+    n = asm["g"].shape[0]
+    assert n == 100
+    for j in range(n):
+        fx, i = _fixture_instance(asm["src"][j])
+        qp = mpc_qp.build_qp(fx["Ad"][i], fx["Bd"][i], fx["gd"][i], fx["x0"][i], fx["xref"][i].T,
+                             fx["contact"][i])
+        for key in ("g", "lba", "uba", "lbx", "ubx"):
+            ref, mine = asm[key][j], qp[key]
+            fin = np.isfinite(ref)
+            assert np.array_equal(fin, np.isfinite(mine)), (j, key)
+            assert np.array_equal(ref[~fin], mine[~fin]), (j, key)
+            scale = max(1.0, float(np.max(np.abs(ref[fin])))) if fin.any() else 1.0
+            assert np.max(np.abs(ref[fin] - mine[fin]), initial=0.0) <= 1e-14 * scale, (j, key)
+        assert np.array_equal(asm["H"], qp["h"].toarray())
+
+
+def test_qp_assembly_matrix_matches_reference_run():
+    """A (_assemble_A_matrix + _precompute_friction_matrix + the SX dyn_builder,
+    :287-359): the reference's structural pattern (5168 entries) and values equal the oracle's."""
+    asm = _assembly()
+    for j in range(asm["A_vals"].shape[0]):
+        fx, i = _fixture_instance(asm["src"][j])
+        Aref = _ref_A(asm, j)
+        Aor = mpc_qp.constraint_matrix(fx["Ad"][i], fx["Bd"][i])
+        assert Aref.nnz == Aor.nnz == 5168
+        Aor_c = Aor.tocoo()
+        po = set(zip(Aor_c.row.tolist(), Aor_c.col.tolist()))
+        Aref_c = Aref.tocoo()
+        assert po == set(zip(Aref_c.row.tolist(), Aref_c.col.tolist()))
+        assert np.max(np.abs(Aref.toarray() - Aor.toarray())) <= 1e-15
+
+
+def test_certified_optimum_is_the_reference_qps_optimum():
+    """The golden primal/dual pairs are KKT points of the QP the REFERENCE assembled (not only
+    of the oracle's restatement): with H, g, A, lba, uba, lbx, ubx from the reference run,
+    stationarity / feasibility / complementarity hold to 1e-8.  The QP is strictly convex, so
+    this pins the parity target to the reference's own problem."""
+    asm = _assembly()
+    for j in range(asm["A_vals"].shape[0]):
+        fx, i = _fixture_instance(asm["src"][j])
+        qp = dict(h=sp.csc_matrix(asm["H"]), a=_ref_A(asm, j), g=asm["g"][j], lba=asm["lba"][j],
+                  uba=asm["uba"][j], lbx=asm["lbx"][j], ubx=asm["ubx"][j])
+        k = mpc_qp.kkt_residuals(qp, fx["w"][i], fx["lam_x"][i], fx["lam_a"][i])
+        assert max(k.values()) < 1e-8, (j, k)
