@@ -99,7 +99,9 @@ class CentroidalMPC:
         self._out = (torch.empty((1, 24 * N), dtype=torch.float32, device=dev),
                      torch.empty((1,), dtype=torch.int32, device=dev),
                      torch.empty((1,), dtype=torch.int32, device=dev))
-        self._y = torch.empty((1, 12 * N), dtype=torch.float32, device=dev)
+        # the reference's multipliers [lam_x (24N) | lam_a (28N)], kept on the device between
+        # ticks for the warm start (cmpc_solve_ref)
+        self._lam = torch.empty((1, 52 * N), dtype=torch.float32, device=dev)
         self._warm = False  # no previous solution yet (the reference's x_prev = None)
         self._print_structure()
 
@@ -133,20 +135,22 @@ class CentroidalMPC:
         t1 = time.perf_counter()
         b = self._buf
         # warm start from the previous tick (centroidal_mpc.py:91-95 with OPTS warm_start_primal
-        # / warm_start_dual): the previous w and cmpc's dual, in place on the device
+        # / warm_start_dual): the previous w and the previous lam_x / lam_a, in place on the
+        # device; the multipliers of this solve come back in the reference layout (:108-110)
         kw = {}
         if self._warm and OPTS["warm_start_primal"]:
             kw["w_init"] = self._out[0]
         if self._warm and OPTS["warm_start_dual"]:
-            kw["y_init"] = self._y
+            kw["lam_init"] = self._lam
         w, st, it = self.plan.solve(b["Ad"], b["Bd"], b["gd"], b["x0"], b["xref"], b["contact"],
-                                    out=self._out, y_out=self._y, **kw)
+                                    out=self._out, lam_out=self._lam, **kw)
         self._warm = True
         w_np = w.cpu().numpy()[0].astype(np.float64)
+        lam = self._lam.cpu().numpy()[0].astype(np.float64)
         status = int(st.cpu().item())
         iters = int(it.cpu().item())
         t2 = time.perf_counter()
-        lam_x, lam_a = _duals.recover(Ad, Bd, gd, x0, xref.T, ct, w_np, self.Q, self.R, MU, FZ_MIN)
+        lam_x, lam_a = lam[:24 * N], lam[24 * N:]
         cost = _duals.cost(w_np, xref.T, self.Q, self.R)
         self.update_time = (t1 - t0) * 1e3
         self.solve_time = (t2 - t1) * 1e3

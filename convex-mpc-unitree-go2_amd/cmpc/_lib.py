@@ -39,7 +39,7 @@ class CParams(ctypes.Structure):
 
 
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
-           "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
+           "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_last_error", "cmpc_version")
 NUM_BINS = 4
 BIN_CAPS = (96, 128, 160, 192)
@@ -71,6 +71,9 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
     if hasattr(lib, "cmpc_solve_warm"):  # absent from A/B builds of older sources
         lib.cmpc_solve_warm.argtypes = [vp, ctypes.c_int64] + [vp] * 13
         lib.cmpc_solve_warm.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_solve_ref"):
+        lib.cmpc_solve_ref.argtypes = [vp, ctypes.c_int64] + [vp] * 13
+        lib.cmpc_solve_ref.restype = ctypes.c_int
     lib.cmpc_build_dynamics.argtypes = [vp, ctypes.c_int64, ctypes.c_float] + [vp] * 8
     lib.cmpc_build_dynamics.restype = ctypes.c_int
     if hasattr(lib, "cmpc_generate_traj"):

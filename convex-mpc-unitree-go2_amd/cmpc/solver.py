@@ -130,7 +130,7 @@ class Plan:
         return list(ms)[:k], list(calls)[:k]
 
     def solve(self, Ad, Bd, gd, x0, xref, contact, out=None, stream=None, w_init=None,
-              y_init=None, y_out=None):
+              y_init=None, y_out=None, lam_init=None, lam_out=None):
         """Solve B instances; all inputs are device tensors (layouts: include/cmpc.h).
 
         Returns (w (B, 24N) fp32, status (B,) int32, iters (B,) int32).  Asynchronous on
@@ -139,7 +139,13 @@ class Plan:
         Warm start (cmpc_solve_warm; the reference's x0 / lam_x0 warm start,
         centroidal_mpc.py:91-95): ``w_init`` (B, 24N) a previous w, ``y_init`` (B, 12N) a
         previous dual.  ``y_out`` (B, 12N) receives the dual at the returned forces; pass
-        ``y_out=True`` to allocate it, in which case the return is (w, status, iters, y)."""
+        ``y_out=True`` to allocate it, in which case the return is (w, status, iters, y).
+
+        Reference multipliers (cmpc_solve_ref; centroidal_mpc.py:91-95, 108-110):
+        ``lam_init`` (B, 52N) warm duals [lam_x | lam_a] in CasADi's layout and convention,
+        ``lam_out`` (B, 52N) the multipliers of the returned point (``lam_out=True``
+        allocates it; the return is then (w, status, iters, lam)).  Not combinable with
+        y_init / y_out."""
         N = self.params.N
         B = Ad.shape[0]
         f32 = torch.float32
@@ -165,6 +171,26 @@ class Plan:
         if stream is None:
             stream = torch.cuda.current_stream(Ad.device)
         sp = ctypes.c_void_p(stream.cuda_stream if hasattr(stream, "cuda_stream") else stream)
+        if lam_init is not None or lam_out is not None:
+            if y_init is not None or y_out is not None:
+                raise ValueError("lam_init/lam_out (reference layout) and y_init/y_out "
+                                 "(cmpc layout) are exclusive")
+            ret_l = lam_out is True
+            if ret_l:
+                lam_out = torch.empty((B, 52 * N), dtype=f32, device=Ad.device)
+            for t, name, shape in ((w_init, "w_init", (B, 24 * N)), (lam_init, "lam_init", (B, 52 * N)),
+                                   (lam_out, "lam_out", (B, 52 * N))):
+                if t is not None:
+                    _dev_tensor(t, name, f32, shape)
+                    self._same_device(t)
+            pt = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None else None)  # noqa: E731
+            with torch.cuda.device(Ad.device):
+                rc = self.lib.cmpc_solve_ref(
+                    self._h, ctypes.c_int64(B),
+                    *[pt(t) for t in (Ad, Bd, gd, x0, xref, contact, w_init, lam_init, w, lam_out,
+                                      status, iters)], sp)
+            _check(self.lib, rc, "cmpc_solve_ref")
+            return (w, status, iters, lam_out) if ret_l else (w, status, iters)
         ret_y = y_out is True
         if ret_y:
             y_out = torch.empty((B, 12 * N), dtype=f32, device=Ad.device)

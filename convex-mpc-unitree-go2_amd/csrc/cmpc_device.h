@@ -32,12 +32,14 @@ struct Inputs {
   const uint8_t* contact;
   const float* w_init;  // nullable: primal warm start, cmpc_solve_warm's w layout
   const float* y_init;  // nullable: dual warm start [B][12N] (force layout)
+  const float* lam_init;  // nullable: the reference's warm duals [B][52N] = [lam_x | lam_a]
 };
 struct Outputs {
   float* w;
   int32_t* status;
   int32_t* iters;
   float* y;             // nullable: the dual at the returned forces [B][12N]
+  float* lam;           // nullable: the reference's multipliers [B][52N] = [lam_x | lam_a]
 };
 
 // Free-variable capacities of the LDS bins (3 forces per stance (step, leg)).

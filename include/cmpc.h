@@ -118,6 +118,25 @@ int cmpc_solve_warm(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd
                     const uint8_t* contact, const float* w_init, const float* y_init,
                     float* w_out, float* y_out, int32_t* status, int32_t* iters, void* stream);
 
+/* Solve with the REFERENCE's multipliers (SURVEY.md 8(b) y_inout; centroidal_mpc.py:91-95
+ * warm start lam_x0 / lam_a0, :108-110 sol["lam_x"] / sol["lam_a"]).  As cmpc_solve, plus:
+ *   w_init    [B][24N]  fp32  nullable; primal warm start, as for cmpc_solve_warm.
+ *   lam_init  [B][52N]  fp32  nullable; warm duals in the reference layout
+ *                             [lam_x (24N: states, then forces) | lam_a (28N: 12N dynamics rows,
+ *                             then 16N friction rows fx-mu fz, -fx-mu fz, fy-mu fz, -fy-mu fz per
+ *                             (step, leg))], CasADi's sign convention.  Mapped on the device to
+ *                             this solver's force dual y = F' lam_fric + lam_x[u].
+ *   lam_out   [B][52N]  fp32  nullable; the multipliers of the returned point in the same layout:
+ *                             H w + g + A' lam_a + lam_x = 0 with lam > 0 on active upper and
+ *                             lam < 0 on active lower bounds (lam_a dynamics rows = minus the
+ *                             adjoint of the rollout; friction / fz-bound multipliers from the
+ *                             accepted face set; swing forces lam_x = -(2R u - Bd' lam_eq)).
+ * lam_init may alias lam_out and w_init may alias w_out. */
+int cmpc_solve_ref(cmpc_plan* plan, int64_t B, const float* Ad, const float* Bd, const float* gd,
+                   const float* x0, const float* xref, const uint8_t* contact,
+                   const float* w_init, const float* lam_init, float* w_out, float* lam_out,
+                   int32_t* status, int32_t* iters, void* stream);
+
 void cmpc_plan_destroy(cmpc_plan* plan);
 
 /* QP data on the device: the reference's discrete dynamics

@@ -38,7 +38,9 @@ REPO = HERE.parents[1]
 sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 
+sys.path.insert(0, str(REPO / "tests"))
 from oracle import mpc_qp, tight_solver  # noqa: E402
+from parity_util import input_digest  # noqa: E402
 from cmpc import synth  # noqa: E402
 
 REF = Path("/root/reference/convex_mpc")
@@ -434,6 +436,65 @@ def make_qp_assembly(name: str = "qp_assembly.npz", n_with_A: int = 16):
     print(name, k, "instances;", printed.strip().splitlines()[1:3])
 
 
+def _certify_one(args):
+    Ad, Bd, gd, x0, xref, contact = args
+    qp = mpc_qp.build_qp(Ad, Bd, gd, x0, xref.T, contact)
+    r = tight_solver.solve(qp)
+    k = r["kkt"]
+    assert max(k.values()) < 1e-8, k
+    return r["w"], r["lam_x"], r["lam_a"], [k["stat"], k["prim"], k["comp"]]
+
+
+def _certify(batch, idx, procs=8):
+    import multiprocessing as mp
+    jobs = [tuple(batch[k][i] for k in ("Ad", "Bd", "gd", "x0", "xref", "contact")) for i in idx]
+    with mp.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_certify_one, jobs, chunksize=4)
+    W, LX, LA, KKT = (np.array(x) for x in zip(*res))
+    return W, LX, LA, KKT
+
+
+def make_cfg3_fixture(name: str = "qp_cfg3.npz", per_bin=(128, 256, 127, 1)):
+    """KKT-certified optima of 512 instances of the config-3 batch (synth.make_config(3),
+    65,536 trot + mixed), stratified over the solver's free-variable bins NC 96/128/160/192
+    (all of the batch's NC = 192 instances).  Inputs are regenerated by the GPU test from the
+    deterministic generator (indices + an input digest are stored, not the inputs)."""
+    b = synth.make_config(3)
+    nf = 3 * (b["contact"] != 0).reshape(b["contact"].shape[0], -1).sum(1)
+    bins = np.searchsorted(np.array([96, 128, 160, 192]), nf)
+    rng = np.random.default_rng(42)
+    idx = np.sort(np.concatenate([rng.choice(np.nonzero(bins == q)[0], min(c, int(np.sum(bins == q))),
+                                             replace=False) for q, c in enumerate(per_bin)]))
+    W, LX, LA, KKT = _certify(b, idx)
+    np.savez_compressed(HERE / name, idx=idx, bins=bins[idx], digest=np.array(input_digest(b, idx)),
+                        w=W, lam_x=LX, lam_a=LA, kkt=KKT)
+    print(name, len(idx), "instances, per bin", np.bincount(bins[idx], minlength=4),
+          "max KKT", KKT.max())
+
+
+def make_nc192_fixture(name: str = "qp_nc192.npz", want: int = 64):
+    """KKT-certified instances of the heaviest bin (more than 160 free forces: > 53 of the 64
+    (step, leg) pairs in stance), collected from config-2-distribution batches
+    (synth.make_batch(65536, seed, mixed=True), seeds 2000...), inputs stored."""
+    rows = {k: [] for k in ("Ad", "Bd", "gd", "x0", "xref", "contact")}
+    seeds = []
+    seed = 2000
+    while len(seeds) < want:
+        b = synth.make_batch(65536, seed=seed, mixed=True)
+        nf = 3 * (b["contact"] != 0).reshape(65536, -1).sum(1)
+        for i in np.nonzero(nf > 160)[0]:
+            if len(seeds) < want:
+                for k in rows:
+                    rows[k].append(b[k][i])
+                seeds.append([seed, i])
+        seed += 1
+    batch = {k: np.array(v) for k, v in rows.items()}
+    W, LX, LA, KKT = _certify(batch, np.arange(want))
+    np.savez_compressed(HERE / name, cases=np.array(seeds), **batch, w=W, lam_x=LX, lam_a=LA,
+                        kkt=KKT)
+    print(name, want, "instances from", seed - 2000, "batches, max KKT", KKT.max())
+
+
 if __name__ == "__main__":
     make_ref_inputs()
     make_traj_ticks()
@@ -442,3 +503,5 @@ if __name__ == "__main__":
     make_qp_fixture(2, 64, "qp_cfg2.npz")
     make_hard_fixture()
     make_qp_assembly()
+    make_cfg3_fixture()
+    make_nc192_fixture()

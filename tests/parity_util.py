@@ -51,3 +51,14 @@ def feasibility(batch, U, mu=0.8, fz_min=10.0):
     v_st = np.where(ct, np.maximum.reduce([fz_min - fz, np.abs(fx) - mu * fz,
                                            np.abs(fy) - mu * fz, np.zeros_like(fz)]), 0.0)
     return np.maximum(v_sw, v_st).reshape(U.shape[0], -1).max(1)
+
+
+def input_digest(batch, idx):
+    """sha256 of the fp32 boundary inputs of instances `idx` (detects generator drift between
+    the fixture's generation and the test)."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in ("Ad", "Bd", "gd", "x0", "xref"):
+        h.update(np.ascontiguousarray(batch[k][idx], dtype=np.float32).tobytes())
+    h.update(np.ascontiguousarray(batch["contact"][idx], dtype=np.uint8).tobytes())
+    return h.hexdigest()

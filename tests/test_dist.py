@@ -67,3 +67,35 @@ def test_scatter_gather_gloo_world2(B):
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+def test_bench_spawns_ranks_and_shards_config3():
+    """`python bench.py --gpus 2` relaunches itself under torch.distributed.run with 2 ranks
+    (before any GPU call); with the solve stubbed (CMPC_BENCH_DRYRUN=1, gloo) both ranks report,
+    their contiguous slices tile the 65,536-instance config-3 batch, and the timing is the
+    max over ranks of the barrier-bracketed region."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, CMPC_BENCH_DRYRUN="1")
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["ranks_reporting"] == 2
+    assert line["spans"] == [[0, 32768], [32768, 65536]]
+    assert line["solved_per_step"] == 65536 and line["stub_work"] == 65536 * 4
+    assert line["steps"] == 3 and line["warmup"] == 1
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    import sys
+    from pathlib import Path
+    repo = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, CMPC_BENCH_DRYRUN="1", WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -66,7 +66,7 @@ def test_qp_structure_matches_reference_print():
     assert qp["lba"].shape == (448,) and qp["lbx"].shape == (384,)
 
 
-@pytest.mark.parametrize("name", ["qp_cfg1.npz", "qp_cfg2.npz", "qp_hard.npz"])
+@pytest.mark.parametrize("name", ["qp_cfg1.npz", "qp_cfg2.npz", "qp_hard.npz", "qp_nc192.npz"])
 def test_golden_fixtures_are_kkt_certified(name):
     fx = load_fixture(name)
     n = fx["w"].shape[0]
@@ -179,3 +179,18 @@ def test_certified_optimum_is_the_reference_qps_optimum():
                   uba=asm["uba"][j], lbx=asm["lbx"][j], ubx=asm["ubx"][j])
         k = mpc_qp.kkt_residuals(qp, fx["w"][i], fx["lam_x"][i], fx["lam_a"][i])
         assert max(k.values()) < 1e-8, (j, k)
+
+
+def test_cfg3_fixture_is_kkt_certified():
+    """qp_cfg3.npz stores indices into the config-3 generator: the digest matches and a sample
+    of the stored optima are KKT points of the regenerated instances."""
+    from parity_util import input_digest
+    fx = load_fixture("qp_cfg3.npz")
+    b = synth.make_config(3, B=65536)
+    assert input_digest(b, fx["idx"]) == str(fx["digest"])
+    for j in range(0, len(fx["idx"]), 32):
+        i = int(fx["idx"][j])
+        qp = mpc_qp.build_qp(b["Ad"][i], b["Bd"][i], b["gd"][i], b["x0"][i], b["xref"][i].T,
+                             b["contact"][i])
+        k = mpc_qp.kkt_residuals(qp, fx["w"][j], fx["lam_x"][j], fx["lam_a"][j])
+        assert max(k.values()) < 1e-8, (i, k)
