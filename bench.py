@@ -217,8 +217,16 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
     comp = {"bound": "mfma", "achieved": tfs, "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
             "frac": tfs / F32_MATRIX_PEAK_TFS, "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
             "flops_per_solve": fl_q / max(n_q, 1)}
-    if counters:
-        comp["counters"] = counters
+    c = (counters or {}).get(KERNEL_NAMES[q].replace(", ", ","), None) or \
+        (counters or {}).get(KERNEL_NAMES[q], None)
+    if c and c.get("SQ_INSTS_MFMA") and avg[q] > 0:
+        # counted matrix work of this kernel per launch (PMC, profiles/) over its live duration
+        ach = c["SQ_INSTS_MFMA"] * 2048.0 / (avg[q] * 1e-3) / 1e12
+        comp.update(model_achieved=tfs, model_frac=tfs / F32_MATRIX_PEAK_TFS, achieved=ach,
+                    frac=ach / F32_MATRIX_PEAK_TFS,
+                    basis="SQ_INSTS_MFMA x 2048 FLOP (v_mfma_f32_16x16x4_f32) per launch from "
+                          "profiles/r02_counters.json / live kernel time",
+                    mfma_per_launch=c["SQ_INSTS_MFMA"], mfma_busy_frac_pmc=c.get("mfma_busy_frac"))
     return roof, comp
 
 
