@@ -130,6 +130,8 @@ def parse(argv=None):
                     help="added to the workload seed (experiments: average over batches)")
     ap.add_argument("--param", action="append", default=[],
                     help="SolverParams override key=value (experiments)")
+    ap.add_argument("--team", type=int, default=-1,
+                    help="small-batch team mode for B <= this (cmpc_plan_set_team): -1 auto, 0 off")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     a = ap.parse_args(argv)
@@ -300,6 +302,8 @@ def main(argv=None):
     Bs = hi - lo
     max_b = max(GB if args.weak_steps > 0 else Bs, 65536 if (world == 1 and args.sub_configs) else 0)
     plan = Plan(SolverParams(max_batch=max_b, **over), device=dev)
+    if args.team != -1 and hasattr(plan.lib, "cmpc_plan_set_team"):
+        plan.set_team(args.team)
     stream = torch.cuda.current_stream(dev)
     d = to_device_batch(shard, dev)
     w = torch.empty((Bs, 24 * 16), dtype=torch.float32, device=dev)

@@ -40,7 +40,8 @@ class CParams(ctypes.Structure):
 
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
            "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
-           "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_last_error", "cmpc_version")
+           "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_plan_set_team", "cmpc_last_error",
+           "cmpc_version")
 NUM_BINS = 4
 BIN_CAPS = (96, 128, 160, 192)
 # solve kernels (register classes): 0 = bins NC 128 + 96, 1 = bins NC 192 + 160
@@ -94,6 +95,9 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
     lib.cmpc_plan_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_float),
                                           ctypes.POINTER(ctypes.c_int32)]
     lib.cmpc_plan_timing_read.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_plan_set_team"):
+        lib.cmpc_plan_set_team.argtypes = [vp, ctypes.c_int64]
+        lib.cmpc_plan_set_team.restype = ctypes.c_int
     lib.cmpc_last_error.argtypes = []
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_version.argtypes = []

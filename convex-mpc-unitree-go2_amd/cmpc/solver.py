@@ -119,6 +119,12 @@ class Plan:
         _check(self.lib, self.lib.cmpc_plan_set_timing(self._h, int(bool(enable))),
                "cmpc_plan_set_timing")
 
+    def set_team(self, max_batch: int):
+        """Small-batch (team) mode for solves of B <= max_batch: four waves per QP.
+        -1 = automatic (B <= 2 x CUs, the default), 0 = off (cmpc_plan_set_team)."""
+        _check(self.lib, self.lib.cmpc_plan_set_team(self._h, int(max_batch)),
+               "cmpc_plan_set_team")
+
     def timing_read(self):
         """-> (ms_per_kernel[2], calls_per_kernel[2]) of the two solve kernels since the last
         read (kernel 0: bins NC 128 + 96; kernel 1: bins NC 192 + 160, _lib.KERNEL_BINS)."""

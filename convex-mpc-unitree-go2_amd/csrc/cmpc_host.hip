@@ -32,6 +32,10 @@ struct cmpc_plan {
   size_t work_off[kNumGroups];
   size_t slab[kNumGroups];
   int grid[kNumGroups];
+  // team mode (cmpc_team.hip): kTeamWaves waves per QP for batches B <= team_max_batch
+  int grid_team[kNumGroups];
+  size_t slab_team[kNumGroups];
+  int64_t team_max_batch = -1;  // -1: automatic (two instances per CU at most)
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -83,6 +87,18 @@ size_t group_slab(int k) {
 
 KernelFn group_fn(int k) {
   return k == 0 ? cmpc::solve_group_kernel<128, 96> : cmpc::solve_group_kernel<192, 160>;
+}
+
+constexpr int kTeamWaves = 4;
+
+size_t team_slab(int k) {
+  return k == 0 ? std::max(cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB)
+                : std::max(cmpc::TeamCfg<192, kTeamWaves>::SLAB, cmpc::TeamCfg<160, kTeamWaves>::SLAB);
+}
+
+KernelFn team_fn(int k) {
+  return k == 0 ? cmpc::solve_team_kernel<128, 96, kTeamWaves>
+                : cmpc::solve_team_kernel<192, 160, kTeamWaves>;
 }
 }  // namespace
 
@@ -179,8 +195,15 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
 #endif
     pl->grid[k] = nb * cus;
     pl->slab[k] = group_slab(k);
+    int nt = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nt, team_fn(k), 64 * kTeamWaves, 0);
+    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+    if (nt < 1) nt = 1;
+    pl->grid_team[k] = nt * cus;
+    pl->slab_team[k] = team_slab(k);
     pl->work_off[k] = work_floats;
-    work_floats += (size_t)pl->grid[k] * pl->slab[k];
+    work_floats += std::max((size_t)pl->grid[k] * pl->slab[k],
+                            (size_t)pl->grid_team[k] * pl->slab_team[k]);
   }
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
@@ -260,8 +283,9 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
                     cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
 }
 
-static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParams& kp,
-                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
+static int record_launch(cmpc_plan* pl, int k, bool team, hipStream_t s,
+                         const cmpc::KParams& kp, const cmpc::Inputs& in,
+                         const cmpc::Outputs& out, unsigned g) {
   hipError_t e;
   cmpc_plan::Rec rec{nullptr, nullptr, k};
   const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
@@ -277,11 +301,11 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64), 0, s, kp, in, out,
-                     pl->d_lists + (size_t)qa * pl->p.max_batch,
+  hipLaunchKernelGGL(team ? team_fn(k) : group_fn(k), dim3(g), dim3(team ? 64 * kTeamWaves : 64),
+                     0, s, kp, in, out, pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
-                     pl->slab[k]);
+                     team ? pl->slab_team[k] : pl->slab[k]);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "solve_group_kernel launch");
   if (rec_this) {
@@ -307,6 +331,9 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   cmpc::KParams kp = pl->kp;
   // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
+  // small batches: a team of kTeamWaves waves per QP (at most two instances per CU)
+  const int64_t tmax = pl->team_max_batch >= 0 ? pl->team_max_batch : 2LL * pl->cus;
+  const bool team = B <= tmax;
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
@@ -314,13 +341,15 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
-    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, pl->side, kp, in, out, g1);
+    const int gr1 = team ? pl->grid_team[1] : pl->grid[1];
+    const unsigned g1 = (unsigned)(gr1 < B ? gr1 : B);
+    rc = record_launch(pl, 1, team, pl->side, kp, in, out, g1);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
-  const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-  rc = record_launch(pl, 0, st, kp, in, out, g0);
+  const int gr0 = team ? pl->grid_team[0] : pl->grid[0];
+  const unsigned g0 = (unsigned)(gr0 < B ? gr0 : B);
+  rc = record_launch(pl, 0, team, st, kp, in, out, g0);
   if (rc != CMPC_OK) return rc;
   if (big && (e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
     return hip_fail(e, "hipStreamWaitEvent");
@@ -429,6 +458,13 @@ int cmpc_plan_set_timing(cmpc_plan* pl, int enable) {
   return CMPC_OK;
 }
 
+int cmpc_plan_set_team(cmpc_plan* pl, int64_t max_batch) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_team: null plan");
+  if (max_batch < -1) return fail(CMPC_E_INVALID, "cmpc_plan_set_team: max_batch must be >= -1");
+  pl->team_max_batch = max_batch;
+  return CMPC_OK;
+}
+
 int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_kernel, int32_t* calls_per_kernel) {
   if (!pl || !ms_per_kernel || !calls_per_kernel)
     return fail(CMPC_E_INVALID, "cmpc_plan_timing_read: null argument");
@@ -462,10 +498,10 @@ void cmpc_plan_destroy(cmpc_plan* pl) {
 
 #ifdef CMPC_STAMPS
 // diagnostic build only: read and clear the per-phase cycle counters
-int cmpc_debug_stamps(unsigned long long* out16) {
-  hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(cmpc::g_stamps), 16 * sizeof(unsigned long long));
+int cmpc_debug_stamps(unsigned long long* out24) {
+  hipError_t e = hipMemcpyFromSymbol(out24, HIP_SYMBOL(cmpc::g_stamps), 24 * sizeof(unsigned long long));
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyFromSymbol");
-  unsigned long long z[16] = {0};
+  unsigned long long z[24] = {0};
   e = hipMemcpyToSymbol(HIP_SYMBOL(cmpc::g_stamps), z, sizeof(z));
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyToSymbol");
   return CMPC_OK;

@@ -1,0 +1,634 @@
+// cmpc_team.hip -- W WAVES PER QP ("team" mode) for small batches.
+//
+// With one wave per QP a batch of B <= 1,024 instances leaves most of the 1,024 SIMDs idle and
+// every instance's latency is its wave's serial chain (BASELINE config 1: B = 256 on 256 CUs).
+// Team mode gives each QP a workgroup of W waves on W SIMDs of one CU.  Wave 0 (the leader)
+// runs solve_instance's control flow unchanged; waves 1..W-1 (helpers) sit in a command loop and
+// join the leader in the matrix phases, which hold ~70 % of a wave's time:
+//   FACTOR  block-row condensation + 4-pivot block sweep inversion (cmpc_wave.hip 1-2),
+//   SYMV    out = M in,
+//   PSTORE / PLOAD  park / restore the inverse,
+// each wave on its own share of the lower-triangle tiles, held in its registers.
+//
+// Tile ownership: the tile COLUMNS J and TT-1-J form a pair of exactly TT+1 tiles; pair pr goes
+// to wave pr % W as its local pair pr / W.  Local slot l of a pair is tile
+//   (pr + l, pr)              for l <  TT - pr   (column pr, rows pr .. TT-1)
+//   (l - 1, TT - 1 - pr)      for l >= TT - pr   (column TT-1-pr, rows TT-1-pr .. TT-1),
+// so the register array is indexed at compile time and (I, J) are uniform scalars.  Owning
+// whole columns keeps the condensation's G_t chunks (the MFMA B operand of column J) local to
+// the wave: only C_t (the A operand, one row chunk per step) and the sweep's pivot panel go
+// through LDS.
+//
+// Synchronisation: a command is published by the leader in a double-buffered slot and starts at
+// a workgroup barrier; the barriers inside a command depend only on its arguments, so every wave
+// passes the same number of them (no data-dependent barrier counts).  Helpers write only the
+// team block (panel, partial sums, scratch); the leader mutates the instance's LDS image only
+// between commands, while the helpers wait at the next command's barrier.
+//
+// This file is compiled as part of cmpc_wave.hip (single translation unit).
+
+template <int NC, int W>
+struct TeamCfg {
+  static constexpr int TT = NC / 16;
+  static constexpr int NPAIR = TT / 2;
+  static constexpr int PPW = (NPAIR + W - 1) / W;  // column pairs per wave
+  static constexpr int SLOTS = PPW * (TT + 1);     // register tiles per wave
+  static constexpr int SLAB = W * SLOTS * 256;     // park slab of the team (floats)
+  static_assert(TT % 2 == 0, "team mode pairs tile columns");
+};
+
+enum : int { kOpExit = 0, kOpFactor = 1, kOpSymv = 2, kOpParkStore = 3, kOpParkLoad = 4 };
+
+template <int NC, int W>
+struct TeamSmem {
+  int cmd[2][4];                         // op, n, arg1, arg2 (double-buffered by sequence)
+  alignas(16) float pan[2][NC * 4];      // sweep panel, double-buffered by pivot step
+  alignas(16) float ds[NC];              // unit-diagonal scaling of the sweep
+  alignas(16) float partR[NC / 16][NC];  // symv: row sums of tile column J's tiles
+  alignas(16) float partC[NC];           // symv: column sums (J < I tiles) landing in chunk J
+  alignas(16) float scr[W][256];         // per-wave 16 x 16 scratch (diagonal mirror)
+};
+
+// slot geometry: local pair j of wave w, slot l -> tile (I, J); valid iff the pair exists
+template <int NC, int W>
+__device__ __forceinline__ bool team_slot(int w, int j, int l, int& I, int& J) {
+  using T = TeamCfg<NC, W>;
+  const int pr = w + j * W;
+  if (l < T::TT - pr) {
+    I = pr + l;
+    J = pr;
+  } else {
+    I = l - 1;
+    J = T::TT - 1 - pr;
+  }
+  return pr < T::NPAIR;
+}
+
+__device__ __forceinline__ void team_barrier() { __syncthreads(); }
+
+// Pin a loaded value at this point: the LDS reads issued before it complete under ONE wait
+// instead of the scheduler sinking each read to its use, where every read would wait for its
+// own latency (~100 cycles) in a dependent chain.
+__device__ __forceinline__ void pin(f4& v) { asm volatile("" : "+v"(v)); }
+__device__ __forceinline__ void pin(float& v) { asm volatile("" : "+v"(v)); }
+
+// One 4-pivot step of the block sweep (pivots 16 K + 4 sub .. +3): publish the pivot columns
+// from the owned tiles, one barrier, then every wave updates its tiles with one MFMA each.
+template <int NC, int W, int WV>
+__device__ __forceinline__ void team_sweep_step(Smem<NC>& s, TeamSmem<NC, W>& ts,
+                                                f4 (&M)[TeamCfg<NC, W>::SLOTS], int w, int K,
+                                                int sub, int g, int c) {
+  using T = TeamCfg<NC, W>;
+  constexpr int TT = T::TT;
+  const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
+  const int c0 = 4 * sub, k0 = 16 * K + c0;
+  const int pc = c - c0;
+  const bool colw = pc >= 0 && pc < 4, roww = g == sub;
+  float* pb = ts.pan[sub & 1];  // = (4 K + sub) & 1
+  CMPC_T0(t_s0);
+  // publish the 4 pivot columns (P^ = P - I on the pivot rows) from the tiles of column K and
+  // (transposed) of row K
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      if (!team_slot<NC, W>(w, j, l, I, J)) continue;
+      const f4 mm = M[j * (TT + 1) + l];
+      if (J == K) {
+        if (colw) {
+          f4 m = mm;
+          if (I == K) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) m[q] -= (4 * g + q == c) ? 1.f : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pb[(16 * I + 4 * g + q) * 4 + pc] = m[q];
+        }
+      } else if (I == K) {  // J < K
+        if (roww) *reinterpret_cast<f4*>(&pb[(16 * J + c) * 4]) = mm;
+      }
+    }
+  }
+  CMPC_ACC(20, t_s0);
+  CMPC_T0(t_s1);
+  team_barrier();
+  CMPC_ACC(21, t_s1);
+#ifdef CMPC_STAMPS
+  if (w != 0) {  // helpers: their barrier waits, summed over the helper waves
+    const unsigned long long _t1 = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&s.st[23], _t1 - t_s1);
+  }
+#endif
+  CMPC_T0(t_s2);
+  // every LDS read of the step is issued here, ahead of the LDL chain (no branch between
+  // them: a read inside a per-tile branch would wait for its own latency)
+  f4 rr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) rr[i] = *reinterpret_cast<const f4*>(&pb[(k0 + i) * 4]);
+  f4 phs[T::PPW][TT + 1], phj[T::PPW][2];
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+    const int pr = w + j * W;
+    const bool ok = pr < T::NPAIR;  // (a missing pair reads row 0 and is skipped below)
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      team_slot<NC, W>(w, j, l, I, J);
+      phs[j][l] = *reinterpret_cast<const f4*>(&pb[(16 * (ok ? I : 0) + c) * 4]);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int J = ok ? (h ? TT - 1 - pr : pr) : 0;
+      phj[j][h] = *reinterpret_cast<const f4*>(&pb[(16 * J + c) * 4]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pin(rr[i]);
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) pin(phs[j][l]);
+    pin(phj[j][0]);
+    pin(phj[j][1]);
+  }
+  float Dm[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) Dm[i * 4 + jj] = rr[i][jj] + ((i == jj) ? 1.f : 0.f);
+  }
+  const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
+  const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
+  const float i1 = __builtin_amdgcn_rcpf(Dm[5] - l10 * Dm[4]);
+  const float u21 = Dm[9] - l20 * Dm[4], u31 = Dm[13] - l30 * Dm[4];
+  const float l21 = u21 * i1, l31 = u31 * i1;
+  const float i2 = __builtin_amdgcn_rcpf(Dm[10] - l20 * Dm[8] - l21 * u21);
+  const float u32 = Dm[14] - l30 * Dm[8] - l31 * u21;
+  const float l32 = u32 * i2;
+  const float i3 = __builtin_amdgcn_rcpf(Dm[15] - l30 * Dm[12] - l31 * u31 - l32 * u32);
+  const float n10 = -l10, n21 = -l21, n32 = -l32;
+  const float n20 = l21 * l10 - l20, n31 = l32 * l21 - l31;
+  const float n30 = -l30 - l31 * n10 - l32 * n20;
+  const float w0 = g3 ? n30 : g2 ? n20 : g1 ? n10 : 1.f;
+  const float w1 = g3 ? n31 : g2 ? n21 : g1 ? 1.f : 0.f;
+  const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
+  const float w3 = g3 ? 1.f : 0.f;
+  const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+    const int pr = w + j * W;
+    if (pr >= T::NPAIR) continue;
+    float bj[2];  // b = diag(1/dl) Y' operand of the pair's two columns
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f4 ph = phj[j][h];
+      bj[h] = fmaf(w3, ph[3], fmaf(w2, ph[2], fmaf(w1, ph[1], w0 * ph[0]))) * ig;
+    }
+    // padding tiles (I >= TA) are updated too: their panel rows are zero, so is the update
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      const f4 ph = phs[j][l];
+      const float a = -fmaf(w3, ph[3], fmaf(w2, ph[2], fmaf(w1, ph[1], w0 * ph[0])));
+      const float b = (l < TT - pr) ? bj[0] : bj[1];
+      M[j * (TT + 1) + l] = mfma4(a, b, M[j * (TT + 1) + l]);
+    }
+    // -2 on the 4 pivot diagonals (tile (K, K): slot 0 when K == pr, slot TT - pr when
+    // K == TT - 1 - pr)
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      team_slot<NC, W>(w, j, l, I, J);
+      if (I != K || J != K) continue;
+      f4& m = M[j * (TT + 1) + l];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
+    }
+  }
+  CMPC_ACC(22, t_s2);
+}
+
+// ------------------------------------------------------------------------------------------
+// FACTOR: M <- -(H + diag(Rt) + shift)^-1 share of this wave (block-row condensation, then the
+// 4-pivot block sweep; cmpc_wave.hip condense_tiles_bc / invert_tiles restated per slot)
+// ------------------------------------------------------------------------------------------
+template <int NC, int W, int WV>
+__device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, const KParams& P,
+                                            f4 (&M)[TeamCfg<NC, W>::SLOTS], int n, float shift,
+                                            int w_rt) {
+  using T = TeamCfg<NC, W>;
+  // WV >= 0: the wave index is a compile-time constant, so every slot's tile (I, J) is too and
+  // the per-tile tests below fold away (straight-line code per wave)
+  const int w = (WV >= 0) ? WV : uniform(w_rt);
+  constexpr int TT = T::TT;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int N = P.N;
+  n = uniform(n);
+#pragma unroll
+  for (int t = 0; t < T::SLOTS; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
+  float aA[4], aT[4], q2[4];  // A[c][4g + q] (A operand of A X), A[4g + q][c] (of A' X), Q2
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int r = 4 * g + q;
+    aA[q] = (c < 12 && r < 12) ? s.A[c * 12 + r] : 0.f;
+    aT[q] = (c < 12 && r < 12) ? s.A[r * 12 + c] : 0.f;
+    q2[q] = (r < 12 && r == c) ? s.Q2[r] : 0.f;
+  }
+  float* Cs = s.G;  // C_i columns, param-major [p][12]
+  CMPC_T0(t_f0);
+  // ---- backward: P_i (every wave, registers) and C_i = P_i B_i (chunk J written by wave J % W)
+  {
+    f4 Pt = {q2[0], q2[1], q2[2], q2[3]};
+    for (int i = N - 1; i >= 0; --i) {
+      const int p0 = s.off[i], p1 = s.off[i + 1];
+#pragma unroll
+      for (int J = 0; J < TT; ++J) {
+        if (J % W != w) continue;                        // uniform
+        if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
+        const int p = 16 * J + c;
+        f4 bt = {0.f, 0.f, 0.f, 0.f};
+        if (g < 3 && p < n) bt = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+        f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) d = mfma4(Pt[q], bt[q], d);
+        if (g < 3 && p >= p0 && p < p1) *reinterpret_cast<f4*>(&Cs[p * 12 + 4 * g]) = d;
+      }
+      if (i > 0) {
+        f4 y = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y = mfma4(Pt[q], aT[q], y);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z = mfma4(aT[q], y[q], z);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Pt[q] = z[q] + q2[q];
+      }
+    }
+  }
+  team_barrier();  // every C_i in LDS
+  CMPC_ACC(16, t_f0);
+  CMPC_T0(t_f1);
+  // ---- forward: owned column chunks G_t = A G_{t-1} + new columns; rows of step t += C_t' G_t
+  {
+    f4 Gd[T::PPW][2];
+    int kJ[T::PPW][2];
+#pragma unroll
+    for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pr = w + j * W;
+        const int J = h ? TT - 1 - pr : pr;
+        Gd[j][h] = f4{0.f, 0.f, 0.f, 0.f};
+        kJ[j][h] = (pr < T::NPAIR && 16 * J < n) ? uniform(s.par[16 * J]) : N;
+      }
+    }
+    const int g3o = (g < 3) ? 4 * g : 0;  // (g = 3 lanes read a valid address, masked below)
+    for (int t = 0; t < N; ++t) {
+      const int p0 = uniform(s.off[t]), p1 = uniform(s.off[t + 1]);
+      // step t's params lie in at most two row chunks, Ia and Ib; their C rows and the new
+      // B columns of the owned chunks are read together, before any MFMA of the step
+      const int Ia = min(p0 >> 4, TT - 1), Ib = (p1 > p0) ? (p1 - 1) >> 4 : Ia;
+      f4 alo = *reinterpret_cast<const f4*>(&Cs[(16 * Ia + c) * 12 + g3o]);
+      f4 ahi = *reinterpret_cast<const f4*>(&Cs[(16 * Ib + c) * 12 + g3o]);
+      f4 bn[T::PPW][2];
+#pragma unroll
+      for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int pr = w + j * W;
+          const int J = (pr < T::NPAIR) ? (h ? TT - 1 - pr : pr) : 0;
+          bn[j][h] = *reinterpret_cast<const f4*>(&s.Bt[(16 * J + c) * 12 + g3o]);
+        }
+      }
+      pin(alo);
+      pin(ahi);
+#pragma unroll
+      for (int j = 0; j < T::PPW; ++j) {
+        pin(bn[j][0]);
+        pin(bn[j][1]);
+      }
+      {
+        const int pa = 16 * Ia + c, pb_ = 16 * Ib + c;
+        const bool ma = pa >= p0 && pa < p1 && g < 3, mb = pb_ >= p0 && pb_ < p1 && g < 3;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          alo[q] = ma ? alo[q] : 0.f;
+          ahi[q] = mb ? ahi[q] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < T::PPW; ++j) {
+        const int pr = w + j * W;
+        if (pr >= T::NPAIR) continue;  // uniform
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int J = h ? TT - 1 - pr : pr;
+          if (t > 0 && kJ[j][h] < t) {
+            f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) d = mfma4(aA[q], Gd[j][h][q], d);
+            Gd[j][h] = d;
+          }
+          const int p = 16 * J + c;
+          if (p >= p0 && p < p1 && g < 3) Gd[j][h] = bn[j][h];
+        }
+#pragma unroll
+        for (int l = 0; l <= TT; ++l) {
+          int I, J;
+          team_slot<NC, W>(w, j, l, I, J);
+          if (I != Ia && I != Ib) continue;  // uniform: rows of step t (none if p1 == p0)
+          if (p1 == p0) continue;
+          const f4 a = (I == Ia) ? alo : ahi;
+          const f4 gj = (l < TT - pr) ? Gd[j][0] : Gd[j][1];
+          f4 acc = M[j * (TT + 1) + l];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc = mfma4(a[q], gj[q], acc);
+          M[j * (TT + 1) + l] = acc;
+        }
+      }
+    }
+  }
+  CMPC_ACC(17, t_f1);
+  CMPC_T0(t_f2);
+  // ---- diagonal tiles: entry (r, c) with step(c) > step(r) is the mirror of (c, r); then
+  // + diag(Rt) + shift, identity on padding; the sweep's scaling from the diagonals
+  float* scr = ts.scr[w];
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      if (!team_slot<NC, W>(w, j, l, I, J)) continue;  // uniform
+      f4 v = M[j * (TT + 1) + l];
+      if (I == J && 16 * I < n) {
+        WSYNC();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) scr[(4 * g + q) * 16 + c] = v[q];
+        WSYNC();
+        const int pc = 16 * I + c;
+        const int kc = (pc < n) ? s.par[pc] : N;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int pr_ = 16 * I + 4 * g + q;
+          const int kr = (pr_ < n) ? s.par[pr_] : N;
+          if (kc > kr) v[q] = scr[c * 16 + 4 * g + q];
+        }
+      }
+      const int col = 16 * J + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
+        else if (row == col) v[q] += s.Rt[row] + shift;
+      }
+      M[j * (TT + 1) + l] = v;
+      if (I == J) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int p = 16 * I + c;
+          if (4 * g + q == c) ts.ds[p] = (p < n && v[q] > 0.f) ? rsqrtf(v[q]) : 1.f;
+        }
+      }
+    }
+  }
+  team_barrier();  // scaling complete
+  CMPC_ACC(18, t_f2);
+  CMPC_T0(t_f3);
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      if (!team_slot<NC, W>(w, j, l, I, J)) continue;
+      const f4 ri = *reinterpret_cast<const f4*>(&ts.ds[16 * I + 4 * g]);
+      const float cj = ts.ds[16 * J + c];
+      f4& m = M[j * (TT + 1) + l];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
+    }
+  }
+  // ---- block sweep, four pivots per step, one barrier per step (double-buffered panel)
+  const int ng = (n + 3) >> 2;
+  if constexpr (WV >= 0) {  // K unrolled: the owned tiles of column K / row K are known
+#pragma unroll
+    for (int K = 0; K < TT; ++K) {
+      if (4 * K >= ng) continue;  // uniform
+      const int subs = (ng - 4 * K) < 4 ? (ng - 4 * K) : 4;
+      for (int sub = 0; sub < subs; ++sub) team_sweep_step<NC, W, WV>(s, ts, M, w, K, sub, g, c);
+    }
+  } else {
+    for (int kk = 0; kk < ng; ++kk) team_sweep_step<NC, W, WV>(s, ts, M, w, kk >> 2, kk & 3, g, c);
+  }
+  CMPC_ACC(19, t_f3);
+  // M holds -(scaled inverse): undo sign and scaling
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      if (!team_slot<NC, W>(w, j, l, I, J)) continue;
+      const f4 ri = *reinterpret_cast<const f4*>(&ts.ds[16 * I + 4 * g]);
+      const float cj = -ts.ds[16 * J + c];
+      f4& m = M[j * (TT + 1) + l];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// SYMV: this wave's partial sums of out = M in (M symmetric, lower tiles stored).  Row sums of
+// tile (I, J) go to partR[J][rows of chunk I] (each written by the column's owner exactly once),
+// the transposed contributions of the J < I tiles to partC[chunk J].  The leader adds them up
+// after the command's barrier in a fixed order (deterministic).
+// ------------------------------------------------------------------------------------------
+template <int NC, int W, int WV>
+__device__ __forceinline__ void team_symv_part(TeamSmem<NC, W>& ts,
+                                               const f4 (&M)[TeamCfg<NC, W>::SLOTS], int n,
+                                               const float* in, int w_rt) {
+  using T = TeamCfg<NC, W>;
+  const int w = (WV >= 0) ? WV : uniform(w_rt);
+  constexpr int TT = T::TT;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  n = uniform(n);
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+    const int pr = w + j * W;
+    if (pr >= T::NPAIR) continue;
+    // all reads first (in[] has NC entries; entries at or past n count as zero).  Padding
+    // tiles (rows >= n) are included: their products are zero, and the leader ignores them.
+    float xc[2], cacc[2] = {0.f, 0.f};
+    f4 xr[TT + 1];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int J = h ? TT - 1 - pr : pr;
+      const float v = in[16 * J + c];
+      xc[h] = (16 * J + c < n) ? v : 0.f;
+    }
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      team_slot<NC, W>(w, j, l, I, J);
+      xr[l] = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xr[l][q] = (16 * I + 4 * g + q < n) ? xr[l][q] : 0.f;
+    }
+    pin(xc[0]);
+    pin(xc[1]);
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) pin(xr[l]);
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      team_slot<NC, W>(w, j, l, I, J);
+      const bool h1 = !(l < TT - pr);
+      const f4 m = M[j * (TT + 1) + l];
+      const float xj = h1 ? xc[1] : xc[0];
+      f4 rs;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rs[q] = row16_sum(m[q] * xj);
+      if (c == 0) *reinterpret_cast<f4*>(&ts.partR[J][16 * I + 4 * g]) = rs;
+      float cp = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cp = fmaf(m[q], xr[l][q], cp);
+      cp = (J < I) ? cp : 0.f;  // the diagonal tile is stored in full: row sums only
+      if (h1) cacc[1] += cp; else cacc[0] += cp;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int J = h ? TT - 1 - pr : pr;
+      const float cs = col4_sum(cacc[h]);
+      if (g == 0) ts.partC[16 * J + c] = cs;
+    }
+  }
+}
+
+// leader side: out[p] = partC[p] + sum_{J <= p/16} partR[J][p] over the first TA chunks, 0 beyond
+template <int NC, int W>
+__device__ __forceinline__ void team_symv_reduce(TeamSmem<NC, W>& ts, int n, float* out) {
+  constexpr int TT = NC / 16;
+  const int lane = opaque_lane();
+  n = uniform(n);
+  const int TA = (n + 15) >> 4;
+  for (int p = lane; p < NC; p += 64) {
+    const int I = p >> 4;
+    float acc = ts.partC[p];
+#pragma unroll
+    for (int J = 0; J < TT; ++J) {
+      const float v = ts.partR[J][p];
+      acc += (J <= I) ? v : 0.f;
+    }
+    out[p] = (I < TA) ? acc : 0.f;
+  }
+  WSYNC();
+}
+
+template <int NC, int W, int WV>
+__device__ __forceinline__ void team_park_store(float* __restrict__ park,
+                                                const f4 (&M)[TeamCfg<NC, W>::SLOTS], int w_rt) {
+  const int w = (WV >= 0) ? WV : uniform(w_rt);
+  const int lane = opaque_lane();
+  float* base = park + (size_t)w * TeamCfg<NC, W>::SLOTS * 256;
+#pragma unroll
+  for (int t = 0; t < TeamCfg<NC, W>::SLOTS; ++t)
+    *reinterpret_cast<f4*>(&base[t * 256 + lane * 4]) = M[t];
+}
+
+template <int NC, int W, int WV>
+__device__ __forceinline__ void team_park_load(const float* __restrict__ park,
+                                               f4 (&M)[TeamCfg<NC, W>::SLOTS], int w_rt) {
+  const int w = (WV >= 0) ? WV : uniform(w_rt);
+  const int lane = opaque_lane();
+  const float* base = park + (size_t)w * TeamCfg<NC, W>::SLOTS * 256;
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < TeamCfg<NC, W>::SLOTS; ++t)
+    M[t] = *reinterpret_cast<const f4*>(&base[t * 256 + lane * 4]);
+}
+
+// ------------------------------------------------------------------------------------------
+// leader: publish a command (wave 0, lane 0) and start it at the barrier
+// ------------------------------------------------------------------------------------------
+template <int NC, int W>
+__device__ __forceinline__ void team_issue(TeamSmem<NC, W>& ts, int& seq, int op, int a0, int a1,
+                                           int a2) {
+  const int lane = opaque_lane();
+  WSYNC();
+  if (lane == 0) {
+    int* cm = ts.cmd[seq & 1];
+    cm[0] = op;
+    cm[1] = a0;
+    cm[2] = a1;
+    cm[3] = a2;
+  }
+  ++seq;
+  team_barrier();
+}
+
+// helpers: execute the leader's commands until kOpExit (one bin's drain loop)
+template <int NC, int W, int WV>
+__device__ __forceinline__ void team_helper(Smem<NC>& s, TeamSmem<NC, W>& ts, const KParams& P,
+                                            float* __restrict__ park, int& seq) {
+  constexpr int w = WV;
+  f4 M[TeamCfg<NC, W>::SLOTS];
+#pragma unroll
+  for (int t = 0; t < TeamCfg<NC, W>::SLOTS; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
+  for (;;) {
+    team_barrier();
+    const int* cm = ts.cmd[seq & 1];
+    const int op = uniform(cm[0]), a0 = uniform(cm[1]), a1 = uniform(cm[2]);
+    ++seq;
+    if (op == kOpExit) break;
+    if (op == kOpFactor) {
+      team_factor<NC, W, WV>(s, ts, P, M, a0, __int_as_float(a1), w);
+    } else if (op == kOpSymv) {
+      const float* in = reinterpret_cast<const float*>(reinterpret_cast<const char*>(&s) + a1);
+      team_symv_part<NC, W, WV>(ts, M, a0, in, w);
+      team_barrier();  // partial sums complete (the leader reduces)
+    } else if (op == kOpParkStore) {
+      team_park_store<NC, W, WV>(park, M, w);
+    } else if (op == kOpParkLoad) {
+      team_park_load<NC, W, WV>(park, M, w);
+    }
+  }
+}
+
+// leader wrappers used by solve_instance
+template <int NC, int W>
+__device__ __forceinline__ void team_factor_lead(Smem<NC>& s, TeamSmem<NC, W>& ts, int& seq,
+                                                 const KParams& P,
+                                                 f4 (&M)[TeamCfg<NC, W>::SLOTS], int n,
+                                                 float shift) {
+  team_issue<NC, W>(ts, seq, kOpFactor, n, __float_as_int(shift), 0);
+  team_factor<NC, W, 0>(s, ts, P, M, n, shift, 0);
+}
+
+template <int NC, int W>
+__device__ __forceinline__ void team_symv_lead(Smem<NC>& s, TeamSmem<NC, W>& ts, int& seq,
+                                               const f4 (&M)[TeamCfg<NC, W>::SLOTS], int n,
+                                               const float* in, float* out) {
+  CMPC_T0(t_sv);
+  const int off = (int)(reinterpret_cast<const char*>(in) - reinterpret_cast<const char*>(&s));
+  team_issue<NC, W>(ts, seq, kOpSymv, n, off, 0);
+  team_symv_part<NC, W, 0>(ts, M, n, in, 0);
+  team_barrier();
+  team_symv_reduce<NC, W>(ts, n, out);
+  CMPC_ACC(3, t_sv);
+  CMPC_CNT(13, 1);
+}
+
+// helpers 1..W-1, each with its wave index as a compile-time constant
+template <int NCA, int NCB, int W, int WV>
+__device__ __forceinline__ void team_helpers(Smem<NCA>& sa, TeamSmem<NCA, W>& ta, Smem<NCB>& sb,
+                                             TeamSmem<NCB, W>& tb, const KParams& P,
+                                             float* __restrict__ park, int w, int& seq) {
+  if constexpr (WV < W) {
+    if (w == WV) {
+      team_helper<NCA, W, WV>(sa, ta, P, park, seq);
+      team_helper<NCB, W, WV>(sb, tb, P, park, seq);
+    } else {
+      team_helpers<NCA, NCB, W, WV + 1>(sa, ta, sb, tb, P, park, w, seq);
+    }
+  }
+}

@@ -129,7 +129,7 @@ __device__ __forceinline__ float col4_sum(float v) {
 // addresses locally instead of the persistent loops hoisting them (and spilling them) for the
 // whole instance.
 __device__ __forceinline__ int opaque_lane() {
-  int l = threadIdx.x;
+  int l = threadIdx.x & 63;
   asm volatile("" : "+v"(l));
   return l;
 }
@@ -146,7 +146,7 @@ __device__ __forceinline__ int opaque_lane() {
 // 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls.
 // ------------------------------------------------------------------------------------------
 #ifdef CMPC_STAMPS
-__device__ unsigned long long g_stamps[16];
+__device__ unsigned long long g_stamps[24];
 // (fenced: outstanding memory and LDS traffic completes, no code moves across a stamp; totals
 // accumulate per wave in LDS, so no contended atomic sits between two stamps)
 #define CMPC_FENCE()                                            \
@@ -216,7 +216,7 @@ constexpr float kLooseTol = 5.f;
 template <int NC>
 struct Smem {
 #ifdef CMPC_STAMPS
-  unsigned long long st[16];       // per-wave stamp totals (flushed to g_stamps at exit)
+  unsigned long long st[24];       // per-wave stamp totals (flushed to g_stamps at exit)
 #endif
   alignas(16) float Bt[NC * 12];   // param-space input matrix, column p at Bt[12p .. 12p+11]
   alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
@@ -1226,8 +1226,10 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
     M[t] = *reinterpret_cast<const f4*>(&park[t * 256 + lane * 4]);
 }
 
+#include "cmpc_team.hip"  // W waves per QP for small batches (leader + helpers)
+
 // ------------------------------------------------------------------------------------------
-// one QP instance on one wave
+// one QP instance on one wave (W = 1) or led by wave 0 of a W-wave team (cmpc_team.hip)
 // A polish session starts from the face set in s.code: record it as the session's first tried
 // set and look it up among the starting sets of failed sessions.  Returns the session's repair
 // budget (none for a remembered set).
@@ -1270,12 +1272,14 @@ __device__ __forceinline__ bool tried_before(Smem<NC>& s, int ntri, int ntried) 
 }
 
 // ------------------------------------------------------------------------------------------
-template <int NC>
+template <int NC, int W>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
-                                               float* __restrict__ park) {
-  using C = Cfg<NC>;
-  f4 M[C::NTL];
+                                               float* __restrict__ park, TeamSmem<NC, W>* ts,
+                                               int* seq) {
+  // W = 1: the whole lower triangle in this wave's registers; W > 1: this wave's team slots
+  f4 M[TeamCfg<NC, W>::SLOTS];
+  static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
   const int lane = opaque_lane();
   const int N = P.N;
   const int NP = 12 * N;
@@ -1433,12 +1437,18 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #ifdef CMPC_DIAG_COUNTS
       ++dg_fact;
 #endif
-      CMPC_T0(t_c);
-      condense_tiles<NC>(s, P, M, nact, uniformf(shift));
-      CMPC_ACC(0, t_c);
-      CMPC_T0(t_i);
-      invert_tiles<NC>(s, M, nact);
-      CMPC_ACC(1, t_i);
+      if constexpr (W == 1) {
+        CMPC_T0(t_c);
+        condense_tiles<NC>(s, P, M, nact, uniformf(shift));
+        CMPC_ACC(0, t_c);
+        CMPC_T0(t_i);
+        invert_tiles<NC>(s, M, nact);
+        CMPC_ACC(1, t_i);
+      } else {
+        CMPC_T0(t_c);
+        team_factor_lead<NC, W>(s, *ts, *seq, P, M, nact, uniformf(shift));
+        CMPC_ACC(0, t_c);
+      }
       refactor = false;
     }
     if (in_polish) {
@@ -1449,7 +1459,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       float step = 3.0e38f, prev = 3.0e38f;
       for (int q = 0; q < CMPC_REFINE_N + kRefineExtra; ++q) {
         gradient<NC>(s, P, nact, s.v, s.g);
-        symv<NC>(s, M, nact, s.g, s.dl);
+        if constexpr (W == 1) symv<NC>(s, M, nact, s.g, s.dl);
+        else team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
         float m = 0.f, mv = 1.f;
         for (int p = lane; p < nact; p += 64) {
           const float vn = s.v[p] - s.dl[p];
@@ -1523,7 +1534,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       }
       shift = uniformf(P.sigma + rho);
       if (parked) {
-        park_load<NC>(park, M);
+        if constexpr (W == 1) {
+          park_load<NC>(park, M);
+        } else {
+          team_issue<NC, W>(*ts, *seq, kOpParkLoad, 0, 0, 0);
+          team_park_load<NC, W, 0>(park, M, 0);
+        }
       } else {
         refactor = true;  // M holds the polish inverse: refactor before the next iteration
         continue;
@@ -1544,7 +1560,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         }
       }
     }
-    symv<NC>(s, M, n, s.r, s.dl);
+    if constexpr (W == 1) symv<NC>(s, M, n, s.r, s.dl);
+    else team_symv_lead<NC, W>(s, *ts, *seq, M, n, s.r, s.dl);
     CMPC_T0(t_rest);
     const bool last = (it == P.max_iter);
     const bool adapt = P.adaptive_interval > 0 && (it % P.adaptive_interval) == 0;
@@ -1628,7 +1645,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // session (most instances pass it; the few that fail refactor once).  HBM writes of a
       // config-3 step drop from ~36 KB to a few hundred bytes per instance at unchanged speed.
       parked = !refactor && !rho_low && nfail > 0;
-      if (parked) park_store<NC>(park, M);  // restored if the polish fails
+      if (parked) {  // restored if the polish fails
+        if constexpr (W == 1) {
+          park_store<NC>(park, M);
+        } else {
+          team_issue<NC, W>(*ts, *seq, kOpParkStore, 0, 0, 0);
+          team_park_store<NC, W, 0>(park, M, 0);
+        }
+      }
 #else
       parked = false;      // a failed polish refactors the ADMM matrix instead
 #endif
@@ -1744,11 +1768,13 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 }
 
 // Drain one bin's queue with this wave (persistent: instance ids come from a device counter).
-template <int NC>
+// (W > 1: the leader's loop; the helpers leave their command loop at the closing kOpExit)
+template <int NC, int W>
 __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const Inputs& in,
                                           const Outputs& out, const int* __restrict__ list,
                                           const int* __restrict__ count, int* __restrict__ head,
-                                          float* __restrict__ park) {
+                                          float* __restrict__ park, TeamSmem<NC, W>* ts = nullptr,
+                                          int* seq = nullptr) {
   const int lane = opaque_lane();
   WSYNC();
   if (lane < 12) {  // KParams copies (each bin's Smem layout places them differently)
@@ -1761,8 +1787,9 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
     if (lane == 0) idx = atomicAdd(head, 1);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= total) break;
-    solve_instance<NC>(s, P, (int64_t)list[idx], in, out, park);
+    solve_instance<NC, W>(s, P, (int64_t)list[idx], in, out, park, ts, seq);
   }
+  if constexpr (W > 1) team_issue<NC, W>(*ts, *seq, kOpExit, 0, 0, 0);
 }
 
 // One persistent kernel per register class: bins NCA and NCB share the occupancy (two waves per
@@ -1784,15 +1811,54 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
 #ifdef CMPC_STAMPS
   // st[] is the first member of every Smem<NC>: one set of totals for the wave
   Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(raw);
-  if (threadIdx.x < 16) s0.st[threadIdx.x] = 0;
+  if (threadIdx.x < 24) s0.st[threadIdx.x] = 0;
 #endif
-  drain_bin<NCA>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa, heads + qa,
-                 park);
-  drain_bin<NCB>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
-                 heads + qa - 1, park);
+  drain_bin<NCA, 1>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa,
+                    heads + qa, park);
+  drain_bin<NCB, 1>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
+                    heads + qa - 1, park);
 #ifdef CMPC_STAMPS
   WSYNC();
-  if (threadIdx.x < 16) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
+  if (threadIdx.x < 24) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
+#endif
+}
+
+// Team mode (cmpc_team.hip): one workgroup of W waves per QP, same queues and bins.  Wave 0
+// leads (drain loop + solve_instance), waves 1..W-1 serve its matrix commands; at most two
+// workgroups per CU (<= 256 VGPRs per wave: the tiles are split W ways).
+template <int NCA, int NCB, int W>
+__global__ void __launch_bounds__(64 * W, 2)
+    solve_team_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
+                      const int* __restrict__ list_b, const int* __restrict__ counts,
+                      int* __restrict__ heads, int qa, float* __restrict__ work, size_t slab) {
+  constexpr size_t kS0 = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
+                                                                : sizeof(Smem<NCB>);
+  constexpr size_t kS = (kS0 + 15) & ~size_t(15);
+  constexpr size_t kT = sizeof(TeamSmem<NCA, W>) > sizeof(TeamSmem<NCB, W>)
+                            ? sizeof(TeamSmem<NCA, W>) : sizeof(TeamSmem<NCB, W>);
+#ifndef CMPC_TEAM_LDS_PAD
+#define CMPC_TEAM_LDS_PAD 0
+#endif
+  __shared__ __attribute__((aligned(16))) unsigned char raw[kS + kT + CMPC_TEAM_LDS_PAD];
+  float* park = work + (size_t)blockIdx.x * slab;
+  Smem<NCA>& sa = *reinterpret_cast<Smem<NCA>*>(raw);
+  Smem<NCB>& sb = *reinterpret_cast<Smem<NCB>*>(raw);
+  TeamSmem<NCA, W>& ta = *reinterpret_cast<TeamSmem<NCA, W>*>(raw + kS);
+  TeamSmem<NCB, W>& tb = *reinterpret_cast<TeamSmem<NCB, W>*>(raw + kS);
+  const int w = uniform((int)(threadIdx.x >> 6));
+  int seq = 0;
+#ifdef CMPC_STAMPS
+  if (threadIdx.x < 24) sa.st[threadIdx.x] = 0;
+#endif
+  if (w == 0) {
+    drain_bin<NCA, W>(sa, P, in, out, list_a, counts + qa, heads + qa, park, &ta, &seq);
+    drain_bin<NCB, W>(sb, P, in, out, list_b, counts + qa - 1, heads + qa - 1, park, &tb, &seq);
+  } else {
+    team_helpers<NCA, NCB, W, 1>(sa, ta, sb, tb, P, park, w, seq);
+  }
+#ifdef CMPC_STAMPS
+  __syncthreads();
+  if (threadIdx.x < 24) atomicAdd(&g_stamps[threadIdx.x], sa.st[threadIdx.x]);
 #endif
 }
 

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--lib", default=str(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_stamps.so"))
     ap.add_argument("--warm", action="store_true",
                     help="measure the bench's next-tick warm-start scenario (cold twin first)")
+    ap.add_argument("--team", type=int, default=-1, help="cmpc_plan_set_team (-1 auto, 0 off)")
     ap.add_argument("--only-bin", type=int, default=-1, help="keep only instances of this bin (0-3)")
     a = ap.parse_args()
     import torch
@@ -37,7 +38,8 @@ def main():
         print("instances kept:", a.batch)
     d = to_device_batch(b)
     plan = Plan(SolverParams(max_batch=a.batch))
-    buf = (ctypes.c_ulonglong * 16)()
+    plan.set_team(a.team)
+    buf = (ctypes.c_ulonglong * 24)()
     kw = {}
     if a.warm:
         y0 = torch.empty((a.batch, 12 * 16), dtype=torch.float32, device=d["Ad"].device)
@@ -73,6 +75,11 @@ def report(lib, plan, d, buf, kw, title):
             continue
         print(f"  {nm:28s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
     print(f"  per call: condense {v[0]/v[8]:.0f}  invert {v[1]/v[8]:.0f}  gradient {v[2]/max(v[12],1):.0f} (x{v[12]/n:.1f})  symv {v[3]/max(v[13],1):.0f} (x{v[13]/n:.1f}) cycles")
+    if v[16] + v[19] > 0:
+        print(f"  team factor per call: backward {v[16]/v[8]:.0f}  forward {v[17]/v[8]:.0f}  "
+              f"mirror+scale {v[18]/v[8]:.0f}  sweep {v[19]/v[8]:.0f} cycles")
+        print(f"  team sweep per call: publish {v[20]/v[8]:.0f}  barrier {v[21]/v[8]:.0f}  "
+              f"LDL+MFMA {v[22]/v[8]:.0f} cycles; helpers' barrier waits (sum) {v[23]/v[8]:.0f}")
     print("  status:", dict(zip(*np.unique(st.cpu().numpy(), return_counts=True))))
 
 if __name__ == "__main__":
