@@ -30,12 +30,16 @@ struct cmpc_plan {
   int* d_lists;     // kNumBins * max_batch
   float* d_work;    // per-wave park slabs; group k's region starts at work_off[k] (groups overlap)
   size_t work_off[kNumGroups];
-  size_t slab[kNumGroups];
-  int grid[kNumGroups];
-  // team mode (cmpc_team.hip): kTeamWaves waves per QP for batches B <= team_max_batch
-  int grid_team[kNumGroups];
-  size_t slab_team[kNumGroups];
+  // kernel variants per group: one wave per QP, and (experiment) for the NC >= 160 group at
+  // large batches a team of kHeavyWaves; index 1 is unused
+  int vgrid[kNumGroups][3];
+  size_t vslab[kNumGroups][3];
+  // small batches (B <= team_max_batch): one kernel for all bins, kTeamWaves waves per QP
+  // (cmpc_team.hip), on the caller's stream
+  int team_grid = 0;
+  size_t team_slab = 0;
   int64_t team_max_batch = -1;  // -1: automatic (two instances per CU at most)
+  bool heavy_team = false;
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -80,25 +84,35 @@ int check_device(const cmpc_plan* pl, const char* what) {
 // 2 (NC 160), one wave per SIMD.  qa = the group's first (larger) bin.
 int group_first_bin(int k) { return k == 0 ? 1 : 3; }
 
-size_t group_slab(int k) {
-  return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
-                : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
-}
+constexpr int kTeamWaves = 4;
+#ifndef CMPC_HEAVY_TEAM_W
+#define CMPC_HEAVY_TEAM_W 2
+#endif
+constexpr int kHeavyWaves = CMPC_HEAVY_TEAM_W;
+enum { kOneWave = 0, kTeam = 1, kHeavyTeam = 2 };
 
-KernelFn group_fn(int k) {
+// kernel, threads per block and park slab (floats per block) of group k in variant v
+KernelFn variant_fn(int k, int v) {
+#ifdef CMPC_HEAVY_TEAM_BUILD
+  if (v == kHeavyTeam && k == 1) return cmpc::solve_team_kernel<192, 160, kHeavyWaves>;
+#endif
   return k == 0 ? cmpc::solve_group_kernel<128, 96> : cmpc::solve_group_kernel<192, 160>;
 }
 
-constexpr int kTeamWaves = 4;
-
-size_t team_slab(int k) {
-  return k == 0 ? std::max(cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB)
-                : std::max(cmpc::TeamCfg<192, kTeamWaves>::SLAB, cmpc::TeamCfg<160, kTeamWaves>::SLAB);
+int variant_threads(int k, int v) {
+#ifdef CMPC_HEAVY_TEAM_BUILD
+  if (v == kHeavyTeam && k == 1) return 64 * kHeavyWaves;
+#endif
+  return 64;
 }
 
-KernelFn team_fn(int k) {
-  return k == 0 ? cmpc::solve_team_kernel<128, 96, kTeamWaves>
-                : cmpc::solve_team_kernel<192, 160, kTeamWaves>;
+size_t variant_slab(int k, int v) {
+#ifdef CMPC_HEAVY_TEAM_BUILD
+  if (v == kHeavyTeam && k == 1)
+    return std::max(cmpc::TeamCfg<192, kHeavyWaves>::SLAB, cmpc::TeamCfg<160, kHeavyWaves>::SLAB);
+#endif
+  return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
+                : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
 }
 }  // namespace
 
@@ -183,28 +197,37 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
   size_t work_floats = 0;
   for (int k = 0; k < kNumGroups; ++k) {
+    size_t need = 0;
+    for (int v = 0; v < 3; ++v) {
+      int nb = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, variant_fn(k, v), variant_threads(k, v), 0);
+      if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+      if (nb < 1) nb = 1;
+#ifdef CMPC_STAMPS
+      if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
+        const int c = atoi(cap);
+        if (v == kOneWave && c >= 1 && c < nb) nb = c;
+      }
+#endif
+      pl->vgrid[k][v] = nb * cus;
+      pl->vslab[k][v] = variant_slab(k, v);
+      need = std::max(need, (size_t)pl->vgrid[k][v] * pl->vslab[k][v]);
+    }
+    pl->work_off[k] = work_floats;
+    work_floats += need;
+  }
+  {
     int nb = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc::solve_team_kernel<kTeamWaves>,
+                                                     64 * kTeamWaves, 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
-#ifdef CMPC_STAMPS
-    if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
-      const int c = atoi(cap);
-      if (c >= 1 && c < nb) nb = c;
-    }
-#endif
-    pl->grid[k] = nb * cus;
-    pl->slab[k] = group_slab(k);
-    int nt = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nt, team_fn(k), 64 * kTeamWaves, 0);
-    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
-    if (nt < 1) nt = 1;
-    pl->grid_team[k] = nt * cus;
-    pl->slab_team[k] = team_slab(k);
-    pl->work_off[k] = work_floats;
-    work_floats += std::max((size_t)pl->grid[k] * pl->slab[k],
-                            (size_t)pl->grid_team[k] * pl->slab_team[k]);
+    pl->team_grid = nb * cus;
+    pl->team_slab = std::max({cmpc::TeamCfg<192, kTeamWaves>::SLAB, cmpc::TeamCfg<160, kTeamWaves>::SLAB,
+                              cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB});
+    work_floats = std::max(work_floats, (size_t)pl->team_grid * pl->team_slab);
   }
+  if (const char* ht = getenv("CMPC_HEAVY_TEAM")) pl->heavy_team = atoi(ht) != 0;  // experiment
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
   e = hipMalloc(&pl->d_work, work_floats * sizeof(float));
@@ -283,9 +306,8 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
                     cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
 }
 
-static int record_launch(cmpc_plan* pl, int k, bool team, hipStream_t s,
-                         const cmpc::KParams& kp, const cmpc::Inputs& in,
-                         const cmpc::Outputs& out, unsigned g) {
+static int record_launch(cmpc_plan* pl, int k, int v, hipStream_t s, const cmpc::KParams& kp,
+                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
   hipError_t e;
   cmpc_plan::Rec rec{nullptr, nullptr, k};
   const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
@@ -301,13 +323,43 @@ static int record_launch(cmpc_plan* pl, int k, bool team, hipStream_t s,
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(team ? team_fn(k) : group_fn(k), dim3(g), dim3(team ? 64 * kTeamWaves : 64),
-                     0, s, kp, in, out, pl->d_lists + (size_t)qa * pl->p.max_batch,
+  hipLaunchKernelGGL(variant_fn(k, v), dim3(g), dim3(variant_threads(k, v)), 0, s, kp, in, out,
+                     pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
-                     team ? pl->slab_team[k] : pl->slab[k]);
+                     pl->vslab[k][v]);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "solve_group_kernel launch");
+  if (rec_this) {
+    if ((e = hipEventRecord(rec.b, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    pl->recs.push_back(rec);
+  }
+  return CMPC_OK;
+}
+
+// team mode: one launch for every bin; timed as solve kernel 0 (kernel 1 records no call)
+static int record_team_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams& kp,
+                              const cmpc::Inputs& in, const cmpc::Outputs& out, int64_t B) {
+  hipError_t e;
+  cmpc_plan::Rec rec{nullptr, nullptr, 0};
+  const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
+  if (rec_this) {
+    if (!pl->pool.empty()) {
+      rec = pl->pool.back();
+      pl->pool.pop_back();
+      rec.group = 0;
+    } else {
+      if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+      if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    }
+    if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  const unsigned g = (unsigned)(pl->team_grid < B ? pl->team_grid : B);
+  hipLaunchKernelGGL(cmpc::solve_team_kernel<kTeamWaves>, dim3(g), dim3(64 * kTeamWaves), 0, s,
+                     kp, in, out, pl->d_lists, (int64_t)pl->p.max_batch, pl->d_counters,
+                     pl->d_counters + cmpc::kNumBins, pl->d_work, pl->team_slab);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "solve_team_kernel launch");
   if (rec_this) {
     if ((e = hipEventRecord(rec.b, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     pl->recs.push_back(rec);
@@ -320,20 +372,31 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   int rc = check_device(pl, "cmpc_solve");
   if (rc != CMPC_OK) return rc;
   hipStream_t st = (hipStream_t)stream;
-  hipError_t e = hipMemsetAsync(pl->d_counters, 0, 2 * cmpc::kNumBins * sizeof(int), st);
-  if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-  const int threads = 256;
-  const unsigned blocks = (unsigned)((B + threads - 1) / threads);
-  hipLaunchKernelGGL(cmpc::bin_kernel, dim3(blocks), dim3(threads), 0, st, pl->kp.N, B,
-                     in.contact, pl->d_counters, pl->d_lists, pl->p.max_batch);
-  e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
+  hipError_t e;
+  if (B <= 1024) {  // one workgroup bins the batch and zeroes the queue heads (no memset)
+    hipLaunchKernelGGL(cmpc::bin_small_kernel, dim3(1), dim3(1024), 0, st, pl->kp.N, (int)B,
+                       in.contact, pl->d_counters, pl->d_counters + cmpc::kNumBins, pl->d_lists,
+                       pl->p.max_batch);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "bin_small_kernel launch");
+  } else {
+    e = hipMemsetAsync(pl->d_counters, 0, 2 * cmpc::kNumBins * sizeof(int), st);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+    const int threads = 256;
+    const unsigned blocks = (unsigned)((B + threads - 1) / threads);
+    hipLaunchKernelGGL(cmpc::bin_kernel, dim3(blocks), dim3(threads), 0, st, pl->kp.N, B,
+                       in.contact, pl->d_counters, pl->d_lists, pl->p.max_batch);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "bin_kernel launch");
+  }
   cmpc::KParams kp = pl->kp;
   // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
-  // small batches: a team of kTeamWaves waves per QP (at most two instances per CU)
+  // small batches: a team of kTeamWaves waves per QP (at most two instances per CU), all bins
+  // in one kernel on the caller's stream
   const int64_t tmax = pl->team_max_batch >= 0 ? pl->team_max_batch : 2LL * pl->cus;
-  const bool team = B <= tmax;
+  if (B <= tmax) return record_team_launch(pl, st, kp, in, out, B);
+  const int v1 = pl->heavy_team ? kHeavyTeam : kOneWave;
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
@@ -341,15 +404,15 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
-    const int gr1 = team ? pl->grid_team[1] : pl->grid[1];
+    const int gr1 = pl->vgrid[1][v1];
     const unsigned g1 = (unsigned)(gr1 < B ? gr1 : B);
-    rc = record_launch(pl, 1, team, pl->side, kp, in, out, g1);
+    rc = record_launch(pl, 1, v1, pl->side, kp, in, out, g1);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
-  const int gr0 = team ? pl->grid_team[0] : pl->grid[0];
+  const int gr0 = pl->vgrid[0][kOneWave];
   const unsigned g0 = (unsigned)(gr0 < B ? gr0 : B);
-  rc = record_launch(pl, 0, team, st, kp, in, out, g0);
+  rc = record_launch(pl, 0, kOneWave, st, kp, in, out, g0);
   if (rc != CMPC_OK) return rc;
   if (big && (e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
     return hip_fail(e, "hipStreamWaitEvent");
@@ -498,10 +561,10 @@ void cmpc_plan_destroy(cmpc_plan* pl) {
 
 #ifdef CMPC_STAMPS
 // diagnostic build only: read and clear the per-phase cycle counters
-int cmpc_debug_stamps(unsigned long long* out24) {
-  hipError_t e = hipMemcpyFromSymbol(out24, HIP_SYMBOL(cmpc::g_stamps), 24 * sizeof(unsigned long long));
+int cmpc_debug_stamps(unsigned long long* out32) {
+  hipError_t e = hipMemcpyFromSymbol(out32, HIP_SYMBOL(cmpc::g_stamps), 32 * sizeof(unsigned long long));
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyFromSymbol");
-  unsigned long long z[24] = {0};
+  unsigned long long z[32] = {0};
   e = hipMemcpyToSymbol(HIP_SYMBOL(cmpc::g_stamps), z, sizeof(z));
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyToSymbol");
   return CMPC_OK;

@@ -121,42 +121,41 @@ __device__ __forceinline__ void team_sweep_step(Smem<NC>& s, TeamSmem<NC, W>& ts
   }
 #endif
   CMPC_T0(t_s2);
-  // every LDS read of the step is issued here, ahead of the LDL chain (no branch between
-  // them: a read inside a per-tile branch would wait for its own latency)
+  // the LDS reads of the step are issued together ahead of the LDL chain (no branch between
+  // them: a read inside a per-tile branch would wait for its own latency): the pivot block and
+  // the first pair's panel rows; a further pair (PPW > 1) reads its rows when its turn comes,
+  // so only one pair's rows are live at a time
   f4 rr[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) rr[i] = *reinterpret_cast<const f4*>(&pb[(k0 + i) * 4]);
-  f4 phs[T::PPW][TT + 1], phj[T::PPW][2];
-#pragma unroll
-  for (int j = 0; j < T::PPW; ++j) {
+  f4 phs[TT + 1], phj[2];
+  auto read_pair = [&](int j) {
     const int pr = w + j * W;
     const bool ok = pr < T::NPAIR;  // (a missing pair reads row 0 and is skipped below)
 #pragma unroll
     for (int l = 0; l <= TT; ++l) {
       int I, J;
       team_slot<NC, W>(w, j, l, I, J);
-      phs[j][l] = *reinterpret_cast<const f4*>(&pb[(16 * (ok ? I : 0) + c) * 4]);
+      phs[l] = *reinterpret_cast<const f4*>(&pb[(16 * (ok ? I : 0) + c) * 4]);
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int J = ok ? (h ? TT - 1 - pr : pr) : 0;
-      phj[j][h] = *reinterpret_cast<const f4*>(&pb[(16 * J + c) * 4]);
+      phj[h] = *reinterpret_cast<const f4*>(&pb[(16 * J + c) * 4]);
     }
-  }
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) pin(phs[l]);
+    pin(phj[0]);
+    pin(phj[1]);
+  };
+  read_pair(0);
 #pragma unroll
   for (int i = 0; i < 4; ++i) pin(rr[i]);
-#pragma unroll
-  for (int j = 0; j < T::PPW; ++j) {
-#pragma unroll
-    for (int l = 0; l <= TT; ++l) pin(phs[j][l]);
-    pin(phj[j][0]);
-    pin(phj[j][1]);
-  }
   float Dm[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) Dm[i * 4 + jj] = rr[i][jj] + ((i == jj) ? 1.f : 0.f);
+    for (int jj = 0; jj < 4; ++jj) Dm[i * 4 + jj] = (i == jj) ? rr[i][jj] + 1.f : rr[i][jj];
   }
   const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
   const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
@@ -179,16 +178,17 @@ __device__ __forceinline__ void team_sweep_step(Smem<NC>& s, TeamSmem<NC, W>& ts
   for (int j = 0; j < T::PPW; ++j) {
     const int pr = w + j * W;
     if (pr >= T::NPAIR) continue;
+    if (j > 0) read_pair(j);
     float bj[2];  // b = diag(1/dl) Y' operand of the pair's two columns
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const f4 ph = phj[j][h];
+      const f4 ph = phj[h];
       bj[h] = fmaf(w3, ph[3], fmaf(w2, ph[2], fmaf(w1, ph[1], w0 * ph[0]))) * ig;
     }
     // padding tiles (I >= TA) are updated too: their panel rows are zero, so is the update
 #pragma unroll
     for (int l = 0; l <= TT; ++l) {
-      const f4 ph = phs[j][l];
+      const f4 ph = phs[l];
       const float a = -fmaf(w3, ph[3], fmaf(w2, ph[2], fmaf(w1, ph[1], w0 * ph[0])));
       const float b = (l < TT - pr) ? bj[0] : bj[1];
       M[j * (TT + 1) + l] = mfma4(a, b, M[j * (TT + 1) + l]);
@@ -610,25 +610,38 @@ __device__ __forceinline__ void team_symv_lead(Smem<NC>& s, TeamSmem<NC, W>& ts,
                                                const float* in, float* out) {
   CMPC_T0(t_sv);
   const int off = (int)(reinterpret_cast<const char*>(in) - reinterpret_cast<const char*>(&s));
+  CMPC_T0(t_a);
   team_issue<NC, W>(ts, seq, kOpSymv, n, off, 0);
+  CMPC_ACC(24, t_a);
+  CMPC_T0(t_b);
   team_symv_part<NC, W, 0>(ts, M, n, in, 0);
+  CMPC_ACC(25, t_b);
+  CMPC_T0(t_c);
   team_barrier();
+  CMPC_ACC(26, t_c);
+  CMPC_T0(t_d);
   team_symv_reduce<NC, W>(ts, n, out);
+  CMPC_ACC(27, t_d);
   CMPC_ACC(3, t_sv);
   CMPC_CNT(13, 1);
 }
 
-// helpers 1..W-1, each with its wave index as a compile-time constant
-template <int NCA, int NCB, int W, int WV>
-__device__ __forceinline__ void team_helpers(Smem<NCA>& sa, TeamSmem<NCA, W>& ta, Smem<NCB>& sb,
-                                             TeamSmem<NCB, W>& tb, const KParams& P,
+// helpers 1..W-1, each with its wave index as a compile-time constant; they follow the leader
+// through the four bins (heaviest first, as solve_team_kernel drains them)
+template <int W, int WV>
+__device__ __forceinline__ void team_helpers(Smem<192>& s3, TeamSmem<192, W>& t3, Smem<160>& s2,
+                                             TeamSmem<160, W>& t2, Smem<128>& s1,
+                                             TeamSmem<128, W>& t1, Smem<96>& s0,
+                                             TeamSmem<96, W>& t0, const KParams& P,
                                              float* __restrict__ park, int w, int& seq) {
   if constexpr (WV < W) {
     if (w == WV) {
-      team_helper<NCA, W, WV>(sa, ta, P, park, seq);
-      team_helper<NCB, W, WV>(sb, tb, P, park, seq);
+      team_helper<192, W, WV>(s3, t3, P, park, seq);
+      team_helper<160, W, WV>(s2, t2, P, park, seq);
+      team_helper<128, W, WV>(s1, t1, P, park, seq);
+      team_helper<96, W, WV>(s0, t0, P, park, seq);
     } else {
-      team_helpers<NCA, NCB, W, WV + 1>(sa, ta, sb, tb, P, park, w, seq);
+      team_helpers<W, WV + 1>(s3, t3, s2, t2, s1, t1, s0, t0, P, park, w, seq);
     }
   }
 }

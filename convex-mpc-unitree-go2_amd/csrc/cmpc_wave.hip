@@ -146,7 +146,7 @@ __device__ __forceinline__ int opaque_lane() {
 // 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls.
 // ------------------------------------------------------------------------------------------
 #ifdef CMPC_STAMPS
-__device__ unsigned long long g_stamps[24];
+__device__ unsigned long long g_stamps[32];
 // (fenced: outstanding memory and LDS traffic completes, no code moves across a stamp; totals
 // accumulate per wave in LDS, so no contended atomic sits between two stamps)
 #define CMPC_FENCE()                                            \
@@ -216,7 +216,7 @@ constexpr float kLooseTol = 5.f;
 template <int NC>
 struct Smem {
 #ifdef CMPC_STAMPS
-  unsigned long long st[24];       // per-wave stamp totals (flushed to g_stamps at exit)
+  unsigned long long st[32];       // per-wave stamp totals (flushed to g_stamps at exit)
 #endif
   alignas(16) float Bt[NC * 12];   // param-space input matrix, column p at Bt[12p .. 12p+11]
   alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
@@ -397,7 +397,7 @@ __device__ __forceinline__ void sweep_operands(Smem<NC>& s, int k0, int g, int c
   for (int i = 0; i < 4; ++i) {
     const f4 rrow = *reinterpret_cast<const f4*>(&s.pan[(k0 + i) * 4]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j] + ((i == j) ? 1.f : 0.f);
+    for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = (i == j) ? rrow[j] + 1.f : rrow[j];
   }
   f4 ph[C::TT];
 #pragma unroll
@@ -717,7 +717,7 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
       for (int i = 0; i < 4; ++i) {
         const f4 rrow = *reinterpret_cast<const f4*>(&s.pan[(k0 + i) * 4]);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = rrow[j] + ((i == j) ? 1.f : 0.f);
+        for (int j = 0; j < 4; ++j) Dm[i * 4 + j] = (i == j) ? rrow[j] + 1.f : rrow[j];
       }
       const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
       const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
@@ -855,32 +855,12 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
 //   adjoint  lambda_k = sum_j (A')^{j-k} Q2 e_{j+1} : L <- L + (A')^d shift_-d(L)
 // (Hillis-Steele; the step shift is a DPP row shift, the product three MFMAs whose accumulator
 // is the trajectory itself).  A^d and (A')^d come from repeated squaring in the same layout.
+// powers A^d and (A')^d, d = 1, 2, 4, 8, in accumulator layout over state positions
+// (pw[l][q] = A^(2^l)[state 3g+q][state of position c]); the gradient's scans use them
 template <int NC>
-__device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, const float* vin,
-                                         float* gout) {
-  CMPC_T0(t_gr);
+__device__ __forceinline__ void gradient_powers(Smem<NC>& s, f4 (&pw)[4], f4 (&tw)[4]) {
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
-  const int N = P.N;
-  n = uniform(n);
-  WSYNC();
-  // State positions (as in condense_tiles_fwd): register q of lane group g holds state 3g + q
-  // (q < 3), q = 3 is padding, so every K = 16 product over states is three MFMAs (K = 12).
-  // h_k = B~_k v_k + d~_k for states 3g..3g+2 of step c
-  f4 Et = {0.f, 0.f, 0.f, 0.f};
-  if (c < N) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) Et[q] = s.Dt[12 * c + 3 * g + q];
-    const int p1 = s.off[c + 1];
-    for (int p = s.off[c]; p < p1; ++p) {
-      const float* bt = &s.Bt[p * 12 + 3 * g];
-      const float vp = vin[p];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) Et[q] = fmaf(bt[q], vp, Et[q]);
-    }
-  }
-  // powers: Pd = A^d and Td = (A')^d in accumulator layout over state positions
-  // (Pd[q] = A^d[state 3g+q][state of position c])
   const int sc = ((c & 3) < 3) ? 3 * (c >> 2) + (c & 3) : -1;
   f4 Pd = {0.f, 0.f, 0.f, 0.f}, Td = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -889,7 +869,6 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
     Pd[q] = (sc >= 0) ? s.A[r * 12 + sc] : 0.f;
     Td[q] = (sc >= 0) ? s.A[sc * 12 + r] : 0.f;
   }
-  f4 pw[4], tw[4];  // d = 1, 2, 4, 8
   pw[0] = Pd;
   tw[0] = Td;
 #pragma unroll
@@ -902,6 +881,68 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
     }
     pw[l] = pn;
     tw[l] = tn;
+  }
+}
+
+// LAT (team / latency mode): the powers come precomputed (one set per instance, `pwc`/`twc`),
+// and the per-step B~ v sum is unrolled to the 12 params a step can hold so that its LDS reads
+// issue together (with two busy waves per SIMD the rolled loop measured faster: issue-bound)
+template <int NC, bool LAT = false>
+__device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, const float* vin,
+                                         float* gout, const f4* pwc = nullptr,
+                                         const f4* twc = nullptr) {
+  CMPC_T0(t_gr);
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int N = P.N;
+  n = uniform(n);
+  WSYNC();
+  // State positions (as in condense_tiles_fwd): register q of lane group g holds state 3g + q
+  // (q < 3), q = 3 is padding, so every K = 16 product over states is three MFMAs (K = 12).
+  // h_k = B~_k v_k + d~_k for states 3g..3g+2 of step c
+  f4 Et = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (LAT) {
+    const int cc = (c < N) ? c : 0;
+    const int p0 = s.off[cc], p1 = s.off[cc + 1];
+    float dt[3], bv[12][3], vv[12];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) dt[q] = s.Dt[12 * cc + 3 * g + q];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      const int p = min(p0 + i, NC - 1);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bv[i][q] = s.Bt[p * 12 + 3 * g + q];
+      vv[i] = vin[p];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Et[q] = dt[q];
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {  // (params past the step may hold anything, even NaN: select)
+      const bool ok = p0 + i < p1;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) Et[q] = ok ? fmaf(bv[i][q], vv[i], Et[q]) : Et[q];
+    }
+    if (c >= N) Et = f4{0.f, 0.f, 0.f, 0.f};
+  } else if (c < N) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Et[q] = s.Dt[12 * c + 3 * g + q];
+    const int p1 = s.off[c + 1];
+    for (int p = s.off[c]; p < p1; ++p) {
+      const float* bt = &s.Bt[p * 12 + 3 * g];
+      const float vp = vin[p];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) Et[q] = fmaf(bt[q], vp, Et[q]);
+    }
+  }
+  f4 pw[4], tw[4];  // d = 1, 2, 4, 8
+  if (pwc != nullptr) {  // (a compile-time constant at every call site)
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      pw[l] = pwc[l];
+      tw[l] = twc[l];
+    }
+  } else {
+    gradient_powers<NC>(s, pw, tw);
   }
   // forward scan: E[:, k] += A^d E[:, k - d]  (A operand = (A^d)' = tw)
 #pragma unroll
@@ -1332,6 +1373,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   }
   build_admm_basis<NC>(s, P, Bg, ntri);
   const int n = 3 * ntri;
+  // team mode: the gradient's powers of A once per instance (registers to spare: the tiles are
+  // split over the team)
+  // (NC <= 128 only: the larger bins need those registers for their tiles)
+  constexpr bool kPow = W > 1 && NC <= 128;
+  f4 pw_c[4], tw_c[4];
+  if constexpr (kPow) gradient_powers<NC>(s, pw_c, tw_c);
+  const f4* pwc = kPow ? pw_c : nullptr;
+  const f4* twc = kPow ? tw_c : nullptr;
   // initial rho per bin: the NC = 128 bin (33-42 stance triples, trot-like schedules) converges
   // in fewer iterations from rho0 / 2; its hard instances (a failed polish session) go back to
   // rho0, where they converge as before (cfg1 +6-10 %, cfg2 +1 %; rho0 / 2 for every bin loses
@@ -1458,7 +1507,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // an ill-conditioned face set (internal foot forces weigh only R) contracts slowly
       float step = 3.0e38f, prev = 3.0e38f;
       for (int q = 0; q < CMPC_REFINE_N + kRefineExtra; ++q) {
-        gradient<NC>(s, P, nact, s.v, s.g);
+        gradient<NC, (W > 1)>(s, P, nact, s.v, s.g, pwc, twc);
         if constexpr (W == 1) symv<NC>(s, M, nact, s.g, s.dl);
         else team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
         float m = 0.f, mv = 1.f;
@@ -1477,7 +1526,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           break;
         prev = step;
       }
-      gradient<NC>(s, P, nact, s.v, s.g);  // E, L at the final point
+      gradient<NC, (W > 1)>(s, P, nact, s.v, s.g, pwc, twc);  // E, L at the final point
       bool changed = false, loose = false;
       const bool ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose);
 #ifdef CMPC_TRACE
@@ -1549,7 +1598,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     ++it;
     iters = it;
     // ---- one ADMM iteration ----
-    gradient<NC>(s, P, n, s.x, s.g);
+    gradient<NC, (W > 1)>(s, P, n, s.x, s.g, pwc, twc);
     {
       const int l = opaque_lane();
       if (l < ntri) {
@@ -1669,7 +1718,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       const bool conv = rp <= P.eps_abs + P.eps_rel * np_ && rd <= P.eps_abs + P.eps_rel * nd;
       status = conv ? 2 : -2;
     }
-    gradient<NC>(s, P, n, s.z, s.g);  // E at u = z (the pure rollout when every leg swings)
+    gradient<NC, (W > 1)>(s, P, n, s.z, s.g, pwc, twc);  // E at u = z (the pure rollout when every leg swings)
   }
   CMPC_T0(t_out);
   // ---- outputs: x_{k+1} = e_{k+1} + xref_k, u from the triples (zero on swing legs) ----
@@ -1690,7 +1739,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   if (out.y) {  // dual at the returned forces, in the force layout (zero on swing legs)
     if (polished && n > 0) {  // y = -grad f(u*) (the ADMM fixed point); s.g is the reduced one
       build_admm_basis<NC>(s, P, Bg, ntri);
-      gradient<NC>(s, P, n, s.x, s.g);
+      gradient<NC, (W > 1)>(s, P, n, s.x, s.g, pwc, twc);
     }
     const float* yf = polished ? s.g : s.y;
     const float sg = polished ? -1.f : 1.f;
@@ -1811,7 +1860,7 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
 #ifdef CMPC_STAMPS
   // st[] is the first member of every Smem<NC>: one set of totals for the wave
   Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(raw);
-  if (threadIdx.x < 24) s0.st[threadIdx.x] = 0;
+  if (threadIdx.x < 32) s0.st[threadIdx.x] = 0;
 #endif
   drain_bin<NCA, 1>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa,
                     heads + qa, park);
@@ -1819,47 +1868,96 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
                     heads + qa - 1, park);
 #ifdef CMPC_STAMPS
   WSYNC();
-  if (threadIdx.x < 24) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
+  if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
 #endif
 }
 
-// Team mode (cmpc_team.hip): one workgroup of W waves per QP, same queues and bins.  Wave 0
-// leads (drain loop + solve_instance), waves 1..W-1 serve its matrix commands; at most two
-// workgroups per CU (<= 256 VGPRs per wave: the tiles are split W ways).
-template <int NCA, int NCB, int W>
+// Team mode (cmpc_team.hip): one workgroup of W waves per QP, one kernel for all four bins
+// (heaviest first: the slow instances start first).  Wave 0 leads (drain loop +
+// solve_instance), waves 1..W-1 serve its matrix commands; at most two workgroups per CU
+// (<= 256 VGPRs per wave: the tiles are split W ways, so every bin fits the same class and a
+// small batch needs one launch on the caller's stream, no fork/join).
+template <int W>
 __global__ void __launch_bounds__(64 * W, 2)
-    solve_team_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
-                      const int* __restrict__ list_b, const int* __restrict__ counts,
-                      int* __restrict__ heads, int qa, float* __restrict__ work, size_t slab) {
-  constexpr size_t kS0 = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
-                                                                : sizeof(Smem<NCB>);
+    solve_team_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ lists,
+                      int64_t stride, const int* __restrict__ counts, int* __restrict__ heads,
+                      float* __restrict__ work, size_t slab) {
+  constexpr size_t kS0 = sizeof(Smem<192>);
+  static_assert(sizeof(Smem<192>) >= sizeof(Smem<160>) && sizeof(Smem<160>) >= sizeof(Smem<128>) &&
+                    sizeof(Smem<128>) >= sizeof(Smem<96>), "Smem grows with NC");
   constexpr size_t kS = (kS0 + 15) & ~size_t(15);
-  constexpr size_t kT = sizeof(TeamSmem<NCA, W>) > sizeof(TeamSmem<NCB, W>)
-                            ? sizeof(TeamSmem<NCA, W>) : sizeof(TeamSmem<NCB, W>);
-#ifndef CMPC_TEAM_LDS_PAD
-#define CMPC_TEAM_LDS_PAD 0
-#endif
-  __shared__ __attribute__((aligned(16))) unsigned char raw[kS + kT + CMPC_TEAM_LDS_PAD];
+  constexpr size_t kT = sizeof(TeamSmem<192, W>);
+  static_assert(sizeof(TeamSmem<192, W>) >= sizeof(TeamSmem<160, W>) &&
+                    sizeof(TeamSmem<160, W>) >= sizeof(TeamSmem<128, W>) &&
+                    sizeof(TeamSmem<128, W>) >= sizeof(TeamSmem<96, W>), "TeamSmem grows with NC");
+  __shared__ __attribute__((aligned(16))) unsigned char raw[kS + kT];
   float* park = work + (size_t)blockIdx.x * slab;
-  Smem<NCA>& sa = *reinterpret_cast<Smem<NCA>*>(raw);
-  Smem<NCB>& sb = *reinterpret_cast<Smem<NCB>*>(raw);
-  TeamSmem<NCA, W>& ta = *reinterpret_cast<TeamSmem<NCA, W>*>(raw + kS);
-  TeamSmem<NCB, W>& tb = *reinterpret_cast<TeamSmem<NCB, W>*>(raw + kS);
+  Smem<192>& s3 = *reinterpret_cast<Smem<192>*>(raw);
+  Smem<160>& s2 = *reinterpret_cast<Smem<160>*>(raw);
+  Smem<128>& s1 = *reinterpret_cast<Smem<128>*>(raw);
+  Smem<96>& s0 = *reinterpret_cast<Smem<96>*>(raw);
+  TeamSmem<192, W>& t3 = *reinterpret_cast<TeamSmem<192, W>*>(raw + kS);
+  TeamSmem<160, W>& t2 = *reinterpret_cast<TeamSmem<160, W>*>(raw + kS);
+  TeamSmem<128, W>& t1 = *reinterpret_cast<TeamSmem<128, W>*>(raw + kS);
+  TeamSmem<96, W>& t0 = *reinterpret_cast<TeamSmem<96, W>*>(raw + kS);
   const int w = uniform((int)(threadIdx.x >> 6));
   int seq = 0;
 #ifdef CMPC_STAMPS
-  if (threadIdx.x < 24) sa.st[threadIdx.x] = 0;
+  if (threadIdx.x < 32) s1.st[threadIdx.x] = 0;
 #endif
   if (w == 0) {
-    drain_bin<NCA, W>(sa, P, in, out, list_a, counts + qa, heads + qa, park, &ta, &seq);
-    drain_bin<NCB, W>(sb, P, in, out, list_b, counts + qa - 1, heads + qa - 1, park, &tb, &seq);
+    drain_bin<192, W>(s3, P, in, out, lists + 3 * stride, counts + 3, heads + 3, park, &t3, &seq);
+    drain_bin<160, W>(s2, P, in, out, lists + 2 * stride, counts + 2, heads + 2, park, &t2, &seq);
+    drain_bin<128, W>(s1, P, in, out, lists + stride, counts + 1, heads + 1, park, &t1, &seq);
+    drain_bin<96, W>(s0, P, in, out, lists, counts, heads, park, &t0, &seq);
   } else {
-    team_helpers<NCA, NCB, W, 1>(sa, ta, sb, tb, P, park, w, seq);
+    team_helpers<W, 1>(s3, t3, s2, t2, s1, t1, s0, t0, P, park, w, seq);
   }
 #ifdef CMPC_STAMPS
   __syncthreads();
-  if (threadIdx.x < 24) atomicAdd(&g_stamps[threadIdx.x], sa.st[threadIdx.x]);
+  if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s1.st[threadIdx.x]);
 #endif
+}
+
+// Binning of a small batch (B <= 1024) in one workgroup: counts are written, not accumulated,
+// and the queue heads are zeroed here, so no memset precedes it (one launch less per solve).
+__global__ void __launch_bounds__(1024) bin_small_kernel(int N, int B,
+                                                         const uint8_t* __restrict__ contact,
+                                                         int* __restrict__ counts,
+                                                         int* __restrict__ heads,
+                                                         int* __restrict__ lists, int64_t stride) {
+  __shared__ int wcnt[16][kNumBins];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  int bin = -1;
+  if (t < B) {
+    const uint8_t* c = contact + (int64_t)t * 4 * N;
+    int cnt = 0;
+    for (int i = 0; i < 4 * N; ++i) cnt += c[i] != 0;
+    const int nf = 3 * cnt;
+    bin = kNumBins - 1;
+    for (int q = 0; q < kNumBins; ++q)
+      if (nf <= kBinCap[q]) { bin = q; break; }
+  }
+  unsigned long long mine = 0;
+#pragma unroll
+  for (int q = 0; q < kNumBins; ++q) {
+    const unsigned long long m = __ballot(bin == q);
+    if (bin == q) mine = m;
+    if (lane == 0) wcnt[wv][q] = __popcll(m);
+  }
+  __syncthreads();
+  if (bin >= 0) {
+    int base = 0;
+    for (int v = 0; v < wv; ++v) base += wcnt[v][bin];
+    const int rank = __popcll(mine & ((1ull << lane) - 1ull));
+    lists[(int64_t)bin * stride + base + rank] = t;
+  }
+  if (t < kNumBins) {
+    int total = 0;
+    for (int v = 0; v < 16; ++v) total += wcnt[v][t];
+    counts[t] = total;
+    heads[t] = 0;
+  }
 }
 
 __global__ void __launch_bounds__(256) bin_kernel(int N, int64_t B,

@@ -39,7 +39,7 @@ def main():
     d = to_device_batch(b)
     plan = Plan(SolverParams(max_batch=a.batch))
     plan.set_team(a.team)
-    buf = (ctypes.c_ulonglong * 24)()
+    buf = (ctypes.c_ulonglong * 32)()
     kw = {}
     if a.warm:
         y0 = torch.empty((a.batch, 12 * 16), dtype=torch.float32, device=d["Ad"].device)
@@ -80,6 +80,9 @@ def report(lib, plan, d, buf, kw, title):
               f"mirror+scale {v[18]/v[8]:.0f}  sweep {v[19]/v[8]:.0f} cycles")
         print(f"  team sweep per call: publish {v[20]/v[8]:.0f}  barrier {v[21]/v[8]:.0f}  "
               f"LDL+MFMA {v[22]/v[8]:.0f} cycles; helpers' barrier waits (sum) {v[23]/v[8]:.0f}")
+    if v[25] > 0:
+        print(f"  team symv per call: issue {v[24]/v[13]:.0f}  part {v[25]/v[13]:.0f}  "
+              f"barrier {v[26]/v[13]:.0f}  reduce {v[27]/v[13]:.0f} cycles")
     print("  status:", dict(zip(*np.unique(st.cpu().numpy(), return_counts=True))))
 
 if __name__ == "__main__":
