@@ -30,16 +30,13 @@ struct cmpc_plan {
   int* d_lists;     // kNumBins * max_batch
   float* d_work;    // per-wave park slabs; group k's region starts at work_off[k] (groups overlap)
   size_t work_off[kNumGroups];
-  // kernel variants per group: one wave per QP, and (experiment) for the NC >= 160 group at
-  // large batches a team of kHeavyWaves; index 1 is unused
-  int vgrid[kNumGroups][3];
-  size_t vslab[kNumGroups][3];
+  int grid[kNumGroups];      // persistent grid of each group's one-wave kernel
+  size_t slab[kNumGroups];   // park slab per wave (floats)
   // small batches (B <= team_max_batch): one kernel for all bins, kTeamWaves waves per QP
   // (cmpc_team.hip), on the caller's stream
   int team_grid = 0;
   size_t team_slab = 0;
   int64_t team_max_batch = -1;  // -1: automatic (two instances per CU at most)
-  bool heavy_team = false;
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -85,32 +82,12 @@ int check_device(const cmpc_plan* pl, const char* what) {
 int group_first_bin(int k) { return k == 0 ? 1 : 3; }
 
 constexpr int kTeamWaves = 4;
-#ifndef CMPC_HEAVY_TEAM_W
-#define CMPC_HEAVY_TEAM_W 2
-#endif
-constexpr int kHeavyWaves = CMPC_HEAVY_TEAM_W;
-enum { kOneWave = 0, kTeam = 1, kHeavyTeam = 2 };
 
-// kernel, threads per block and park slab (floats per block) of group k in variant v
-KernelFn variant_fn(int k, int v) {
-#ifdef CMPC_HEAVY_TEAM_BUILD
-  if (v == kHeavyTeam && k == 1) return cmpc::solve_team_kernel<192, 160, kHeavyWaves>;
-#endif
+KernelFn group_fn(int k) {
   return k == 0 ? cmpc::solve_group_kernel<128, 96> : cmpc::solve_group_kernel<192, 160>;
 }
 
-int variant_threads(int k, int v) {
-#ifdef CMPC_HEAVY_TEAM_BUILD
-  if (v == kHeavyTeam && k == 1) return 64 * kHeavyWaves;
-#endif
-  return 64;
-}
-
-size_t variant_slab(int k, int v) {
-#ifdef CMPC_HEAVY_TEAM_BUILD
-  if (v == kHeavyTeam && k == 1)
-    return std::max(cmpc::TeamCfg<192, kHeavyWaves>::SLAB, cmpc::TeamCfg<160, kHeavyWaves>::SLAB);
-#endif
+size_t group_slab(int k) {
   return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
                 : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
 }
@@ -197,24 +174,20 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
   size_t work_floats = 0;
   for (int k = 0; k < kNumGroups; ++k) {
-    size_t need = 0;
-    for (int v = 0; v < 3; ++v) {
-      int nb = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, variant_fn(k, v), variant_threads(k, v), 0);
-      if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
-      if (nb < 1) nb = 1;
+    int nb = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64, 0);
+    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+    if (nb < 1) nb = 1;
 #ifdef CMPC_STAMPS
-      if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
-        const int c = atoi(cap);
-        if (v == kOneWave && c >= 1 && c < nb) nb = c;
-      }
-#endif
-      pl->vgrid[k][v] = nb * cus;
-      pl->vslab[k][v] = variant_slab(k, v);
-      need = std::max(need, (size_t)pl->vgrid[k][v] * pl->vslab[k][v]);
+    if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
+      const int c = atoi(cap);
+      if (c >= 1 && c < nb) nb = c;
     }
+#endif
+    pl->grid[k] = nb * cus;
+    pl->slab[k] = group_slab(k);
     pl->work_off[k] = work_floats;
-    work_floats += need;
+    work_floats += (size_t)pl->grid[k] * pl->slab[k];
   }
   {
     int nb = 0;
@@ -227,7 +200,6 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
                               cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB});
     work_floats = std::max(work_floats, (size_t)pl->team_grid * pl->team_slab);
   }
-  if (const char* ht = getenv("CMPC_HEAVY_TEAM")) pl->heavy_team = atoi(ht) != 0;  // experiment
   e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
   e = hipMalloc(&pl->d_work, work_floats * sizeof(float));
@@ -306,7 +278,7 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
                     cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
 }
 
-static int record_launch(cmpc_plan* pl, int k, int v, hipStream_t s, const cmpc::KParams& kp,
+static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParams& kp,
                          const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
   hipError_t e;
   cmpc_plan::Rec rec{nullptr, nullptr, k};
@@ -323,11 +295,11 @@ static int record_launch(cmpc_plan* pl, int k, int v, hipStream_t s, const cmpc:
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(variant_fn(k, v), dim3(g), dim3(variant_threads(k, v)), 0, s, kp, in, out,
+  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
-                     pl->vslab[k][v]);
+                     pl->slab[k]);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "solve_group_kernel launch");
   if (rec_this) {
@@ -396,7 +368,6 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // in one kernel on the caller's stream
   const int64_t tmax = pl->team_max_batch >= 0 ? pl->team_max_batch : 2LL * pl->cus;
   if (B <= tmax) return record_team_launch(pl, st, kp, in, out, B);
-  const int v1 = pl->heavy_team ? kHeavyTeam : kOneWave;
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
@@ -404,15 +375,13 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
-    const int gr1 = pl->vgrid[1][v1];
-    const unsigned g1 = (unsigned)(gr1 < B ? gr1 : B);
-    rc = record_launch(pl, 1, v1, pl->side, kp, in, out, g1);
+    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+    rc = record_launch(pl, 1, pl->side, kp, in, out, g1);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
-  const int gr0 = pl->vgrid[0][kOneWave];
-  const unsigned g0 = (unsigned)(gr0 < B ? gr0 : B);
-  rc = record_launch(pl, 0, kOneWave, st, kp, in, out, g0);
+  const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
+  rc = record_launch(pl, 0, st, kp, in, out, g0);
   if (rc != CMPC_OK) return rc;
   if (big && (e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
     return hip_fail(e, "hipStreamWaitEvent");

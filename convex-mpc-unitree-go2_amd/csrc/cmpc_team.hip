@@ -44,9 +44,9 @@ struct TeamSmem {
   int cmd[2][4];                         // op, n, arg1, arg2 (double-buffered by sequence)
   alignas(16) float pan[2][NC * 4];      // sweep panel, double-buffered by pivot step
   alignas(16) float ds[NC];              // unit-diagonal scaling of the sweep
-  alignas(16) float partR[NC / 16][NC];  // symv: row sums of tile column J's tiles
+  alignas(16) float partR[NC / 32][NC];  // symv: row sums of column pair pr's tiles
   alignas(16) float partC[NC];           // symv: column sums (J < I tiles) landing in chunk J
-  alignas(16) float scr[W][256];         // per-wave 16 x 16 scratch (diagonal mirror)
+  alignas(16) float scr[W][512];         // per-wave 2 x 16 x 16 scratch (diagonal mirror)
 };
 
 // slot geometry: local pair j of wave w, slot l -> tile (I, J); valid iff the pair exists
@@ -85,7 +85,6 @@ __device__ __forceinline__ void team_sweep_step(Smem<NC>& s, TeamSmem<NC, W>& ts
   const int pc = c - c0;
   const bool colw = pc >= 0 && pc < 4, roww = g == sub;
   float* pb = ts.pan[sub & 1];  // = (4 K + sub) & 1
-  CMPC_T0(t_s0);
   // publish the 4 pivot columns (P^ = P - I on the pivot rows) from the tiles of column K and
   // (transposed) of row K
 #pragma unroll
@@ -110,17 +109,7 @@ __device__ __forceinline__ void team_sweep_step(Smem<NC>& s, TeamSmem<NC, W>& ts
       }
     }
   }
-  CMPC_ACC(20, t_s0);
-  CMPC_T0(t_s1);
   team_barrier();
-  CMPC_ACC(21, t_s1);
-#ifdef CMPC_STAMPS
-  if (w != 0) {  // helpers: their barrier waits, summed over the helper waves
-    const unsigned long long _t1 = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x & 63) == 0) atomicAdd(&s.st[23], _t1 - t_s1);
-  }
-#endif
-  CMPC_T0(t_s2);
   // the LDS reads of the step are issued together ahead of the LDL chain (no branch between
   // them: a read inside a per-tile branch would wait for its own latency): the pivot block and
   // the first pair's panel rows; a further pair (PPW > 1) reads its rows when its turn comes,
@@ -205,7 +194,42 @@ __device__ __forceinline__ void team_sweep_step(Smem<NC>& s, TeamSmem<NC, W>& ts
       for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
     }
   }
-  CMPC_ACC(22, t_s2);
+}
+
+// M_IJ *= sgn diag(ds_I) M_IJ diag(ds_J) on every owned tile (all reads issued first)
+template <int NC, int W>
+__device__ __forceinline__ void team_scale(TeamSmem<NC, W>& ts, f4 (&M)[TeamCfg<NC, W>::SLOTS],
+                                           int w, int g, int c, float sgn) {
+  using T = TeamCfg<NC, W>;
+  constexpr int TT = T::TT;
+#pragma unroll
+  for (int j = 0; j < T::PPW; ++j) {
+    const int pr = w + j * W;
+    if (pr >= T::NPAIR) continue;  // uniform
+    f4 ri[TT];  // rows pr .. TT-1 (index I - pr)
+#pragma unroll
+    for (int r = 0; r < TT; ++r) {
+      const int I = min(pr + r, TT - 1);
+      ri[r] = *reinterpret_cast<const f4*>(&ts.ds[16 * I + 4 * g]);
+    }
+    float c0 = ts.ds[16 * pr + c], c1 = ts.ds[16 * (TT - 1 - pr) + c];
+#pragma unroll
+    for (int r = 0; r < TT; ++r) pin(ri[r]);
+    pin(c0);
+    pin(c1);
+    c0 *= sgn;
+    c1 *= sgn;
+#pragma unroll
+    for (int l = 0; l <= TT; ++l) {
+      int I, J;
+      team_slot<NC, W>(w, j, l, I, J);
+      const f4 rv = ri[I - pr];
+      const float cj = (l < TT - pr) ? c0 : c1;
+      f4& m = M[j * (TT + 1) + l];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] *= rv[q] * cj;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -227,19 +251,24 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
   n = uniform(n);
 #pragma unroll
   for (int t = 0; t < T::SLOTS; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
-  float aA[4], aT[4], q2[4];  // A[c][4g + q] (A operand of A X), A[4g + q][c] (of A' X), Q2
+  // State layout (as condense_tiles_fwd and the gradient): accumulator position 4g + q holds
+  // state 3g + q for q < 3 and is padding for q = 3, so every product over the 12 states is
+  // three v_mfma_f32_16x16x4_f32 (K = 12), not four.  Lane column c holds state sc (or none).
+  const int sc = ((c & 3) < 3) ? 3 * (c >> 2) + (c & 3) : -1;
+  float aA[3], aT[3];  // A[sc][3g + q] (A operand of A X), A[3g + q][sc] (of A' X)
+  f4 q2 = {0.f, 0.f, 0.f, 0.f};  // Q2 in accumulator layout
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = 4 * g + q;
-    aA[q] = (c < 12 && r < 12) ? s.A[c * 12 + r] : 0.f;
-    aT[q] = (c < 12 && r < 12) ? s.A[r * 12 + c] : 0.f;
-    q2[q] = (r < 12 && r == c) ? s.Q2[r] : 0.f;
+  for (int q = 0; q < 3; ++q) {
+    const int r = 3 * g + q;
+    aA[q] = (sc >= 0) ? s.A[sc * 12 + r] : 0.f;
+    aT[q] = (sc >= 0) ? s.A[r * 12 + sc] : 0.f;
+    q2[q] = (r == sc) ? s.Q2[r] : 0.f;
   }
   float* Cs = s.G;  // C_i columns, param-major [p][12]
   CMPC_T0(t_f0);
   // ---- backward: P_i (every wave, registers) and C_i = P_i B_i (chunk J written by wave J % W)
   {
-    f4 Pt = {q2[0], q2[1], q2[2], q2[3]};
+    f4 Pt = q2;
     for (int i = N - 1; i >= 0; --i) {
       const int p0 = s.off[i], p1 = s.off[i + 1];
 #pragma unroll
@@ -247,19 +276,23 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
         if (J % W != w) continue;                        // uniform
         if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
         const int p = 16 * J + c;
-        f4 bt = {0.f, 0.f, 0.f, 0.f};
-        if (g < 3 && p < n) bt = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+        float bt[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bt[q] = s.Bt[p * 12 + 3 * g + q];
         f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) d = mfma4(Pt[q], bt[q], d);
-        if (g < 3 && p >= p0 && p < p1) *reinterpret_cast<f4*>(&Cs[p * 12 + 4 * g]) = d;
+        for (int q = 0; q < 3; ++q) d = mfma4(Pt[q], (p < n) ? bt[q] : 0.f, d);
+        if (p >= p0 && p < p1) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) Cs[p * 12 + 3 * g + q] = d[q];
+        }
       }
       if (i > 0) {
         f4 y = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) y = mfma4(Pt[q], aT[q], y);
+        for (int q = 0; q < 3; ++q) y = mfma4(Pt[q], aT[q], y);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) z = mfma4(aT[q], y[q], z);
+        for (int q = 0; q < 3; ++q) z = mfma4(aT[q], y[q], z);
 #pragma unroll
         for (int q = 0; q < 4; ++q) Pt[q] = z[q] + q2[q];
       }
@@ -282,14 +315,17 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
         kJ[j][h] = (pr < T::NPAIR && 16 * J < n) ? uniform(s.par[16 * J]) : N;
       }
     }
-    const int g3o = (g < 3) ? 4 * g : 0;  // (g = 3 lanes read a valid address, masked below)
     for (int t = 0; t < N; ++t) {
       const int p0 = uniform(s.off[t]), p1 = uniform(s.off[t + 1]);
       // step t's params lie in at most two row chunks, Ia and Ib; their C rows and the new
       // B columns of the owned chunks are read together, before any MFMA of the step
       const int Ia = min(p0 >> 4, TT - 1), Ib = (p1 > p0) ? (p1 - 1) >> 4 : Ia;
-      f4 alo = *reinterpret_cast<const f4*>(&Cs[(16 * Ia + c) * 12 + g3o]);
-      f4 ahi = *reinterpret_cast<const f4*>(&Cs[(16 * Ib + c) * 12 + g3o]);
+      f4 alo = {0.f, 0.f, 0.f, 0.f}, ahi = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        alo[q] = Cs[(16 * Ia + c) * 12 + 3 * g + q];
+        ahi[q] = Cs[(16 * Ib + c) * 12 + 3 * g + q];
+      }
       f4 bn[T::PPW][2];
 #pragma unroll
       for (int j = 0; j < T::PPW; ++j) {
@@ -297,7 +333,9 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
         for (int h = 0; h < 2; ++h) {
           const int pr = w + j * W;
           const int J = (pr < T::NPAIR) ? (h ? TT - 1 - pr : pr) : 0;
-          bn[j][h] = *reinterpret_cast<const f4*>(&s.Bt[(16 * J + c) * 12 + g3o]);
+          bn[j][h] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int q = 0; q < 3; ++q) bn[j][h][q] = s.Bt[(16 * J + c) * 12 + 3 * g + q];
         }
       }
       pin(alo);
@@ -309,9 +347,9 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
       }
       {
         const int pa = 16 * Ia + c, pb_ = 16 * Ib + c;
-        const bool ma = pa >= p0 && pa < p1 && g < 3, mb = pb_ >= p0 && pb_ < p1 && g < 3;
+        const bool ma = pa >= p0 && pa < p1, mb = pb_ >= p0 && pb_ < p1;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < 3; ++q) {
           alo[q] = ma ? alo[q] : 0.f;
           ahi[q] = mb ? ahi[q] : 0.f;
         }
@@ -326,11 +364,11 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
           if (t > 0 && kJ[j][h] < t) {
             f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < 4; ++q) d = mfma4(aA[q], Gd[j][h][q], d);
+            for (int q = 0; q < 3; ++q) d = mfma4(aA[q], Gd[j][h][q], d);
             Gd[j][h] = d;
           }
           const int p = 16 * J + c;
-          if (p >= p0 && p < p1 && g < 3) Gd[j][h] = bn[j][h];
+          if (p >= p0 && p < p1) Gd[j][h] = bn[j][h];
         }
 #pragma unroll
         for (int l = 0; l <= TT; ++l) {
@@ -342,7 +380,7 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
           const f4 gj = (l < TT - pr) ? Gd[j][0] : Gd[j][1];
           f4 acc = M[j * (TT + 1) + l];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc = mfma4(a[q], gj[q], acc);
+          for (int q = 0; q < 3; ++q) acc = mfma4(a[q], gj[q], acc);
           M[j * (TT + 1) + l] = acc;
         }
       }
@@ -351,62 +389,76 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
   CMPC_ACC(17, t_f1);
   CMPC_T0(t_f2);
   // ---- diagonal tiles: entry (r, c) with step(c) > step(r) is the mirror of (c, r); then
-  // + diag(Rt) + shift, identity on padding; the sweep's scaling from the diagonals
+  // + diag(Rt) + shift, identity on padding; the sweep's scaling from the diagonals.  A pair's
+  // two diagonal tiles are slots 0 and TT - pr; their transposes go through the wave's scratch,
+  // and every LDS read of the phase is issued before its first use.
   float* scr = ts.scr[w];
 #pragma unroll
   for (int j = 0; j < T::PPW; ++j) {
+    const int pr = w + j * W;
+    if (pr >= T::NPAIR) continue;  // uniform
+    const int base = j * (TT + 1);
+    const int Jd[2] = {pr, TT - 1 - pr};
+    const int ld[2] = {0, TT - pr};
+    f4 v[2], tr[2];
+    int kc[2], kr[2][4];
+    float rt[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) v[h] = M[base + ld[h]];
+    WSYNC();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) scr[256 * h + (4 * g + q) * 16 + c] = v[h][q];
+    }
+    WSYNC();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int I = Jd[h];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) tr[h][q] = scr[256 * h + c * 16 + 4 * g + q];
+      kc[h] = s.par[16 * I + c];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) kr[h][q] = s.par[16 * I + 4 * g + q];
+      rt[h] = s.Rt[16 * I + c];
+    }
+    WSYNC();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int I = Jd[h];
+      const int pc = 16 * I + c;
+      const int kcv = (pc < n) ? kc[h] : N;
+      f4 m = v[h];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        const int krv = (row < n) ? kr[h][q] : N;
+        if (16 * I < n && kcv > krv) m[q] = tr[h][q];
+        if (row >= n || pc >= n) m[q] = (row == pc) ? 1.f : 0.f;
+        else if (row == pc) m[q] += rt[h] + shift;
+        if (4 * g + q == c) ts.ds[pc] = (pc < n && m[q] > 0.f) ? rsqrtf(m[q]) : 1.f;
+      }
+      M[base + ld[h]] = m;
+    }
+    // off-diagonal tiles: zero where the row or the column is padding
 #pragma unroll
     for (int l = 0; l <= TT; ++l) {
       int I, J;
-      if (!team_slot<NC, W>(w, j, l, I, J)) continue;  // uniform
-      f4 v = M[j * (TT + 1) + l];
-      if (I == J && 16 * I < n) {
-        WSYNC();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) scr[(4 * g + q) * 16 + c] = v[q];
-        WSYNC();
-        const int pc = 16 * I + c;
-        const int kc = (pc < n) ? s.par[pc] : N;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int pr_ = 16 * I + 4 * g + q;
-          const int kr = (pr_ < n) ? s.par[pr_] : N;
-          if (kc > kr) v[q] = scr[c * 16 + 4 * g + q];
-        }
-      }
+      team_slot<NC, W>(w, j, l, I, J);
+      if (I == J) continue;
+      f4& m = M[base + l];
       const int col = 16 * J + c;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int row = 16 * I + 4 * g + q;
-        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
-        else if (row == col) v[q] += s.Rt[row] + shift;
-      }
-      M[j * (TT + 1) + l] = v;
-      if (I == J) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int p = 16 * I + c;
-          if (4 * g + q == c) ts.ds[p] = (p < n && v[q] > 0.f) ? rsqrtf(v[q]) : 1.f;
-        }
+        if (row >= n || col >= n) m[q] = 0.f;
       }
     }
   }
   team_barrier();  // scaling complete
   CMPC_ACC(18, t_f2);
   CMPC_T0(t_f3);
-#pragma unroll
-  for (int j = 0; j < T::PPW; ++j) {
-#pragma unroll
-    for (int l = 0; l <= TT; ++l) {
-      int I, J;
-      if (!team_slot<NC, W>(w, j, l, I, J)) continue;
-      const f4 ri = *reinterpret_cast<const f4*>(&ts.ds[16 * I + 4 * g]);
-      const float cj = ts.ds[16 * J + c];
-      f4& m = M[j * (TT + 1) + l];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
-    }
-  }
+  team_scale<NC, W>(ts, M, w, g, c, 1.f);
   // ---- block sweep, four pivots per step, one barrier per step (double-buffered panel)
   const int ng = (n + 3) >> 2;
   if constexpr (WV >= 0) {  // K unrolled: the owned tiles of column K / row K are known
@@ -421,19 +473,7 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
   }
   CMPC_ACC(19, t_f3);
   // M holds -(scaled inverse): undo sign and scaling
-#pragma unroll
-  for (int j = 0; j < T::PPW; ++j) {
-#pragma unroll
-    for (int l = 0; l <= TT; ++l) {
-      int I, J;
-      if (!team_slot<NC, W>(w, j, l, I, J)) continue;
-      const f4 ri = *reinterpret_cast<const f4*>(&ts.ds[16 * I + 4 * g]);
-      const float cj = -ts.ds[16 * J + c];
-      f4& m = M[j * (TT + 1) + l];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
-    }
-  }
+  team_scale<NC, W>(ts, M, w, g, c, -1.f);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -442,6 +482,11 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
 // the transposed contributions of the J < I tiles to partC[chunk J].  The leader adds them up
 // after the command's barrier in a fixed order (deterministic).
 // ------------------------------------------------------------------------------------------
+// SYMV: this wave's partial sums of out = M in (M symmetric, lower tiles stored).  Row sums of
+// column pair pr's tiles in row chunk I (both columns' tiles of a row summed before the one
+// 16-lane reduction) go to partR[pr][rows of chunk I], written once by the pair's owner; the
+// transposed contributions of the J < I tiles go to partC[chunk J].  The leader adds them up
+// after the command's barrier in a fixed order (deterministic).
 template <int NC, int W, int WV>
 __device__ __forceinline__ void team_symv_part(TeamSmem<NC, W>& ts,
                                                const f4 (&M)[TeamCfg<NC, W>::SLOTS], int n,
@@ -456,58 +501,71 @@ __device__ __forceinline__ void team_symv_part(TeamSmem<NC, W>& ts,
   for (int j = 0; j < T::PPW; ++j) {
     const int pr = w + j * W;
     if (pr >= T::NPAIR) continue;
+    const int J0 = pr, J1 = TT - 1 - pr;
     // all reads first (in[] has NC entries; entries at or past n count as zero).  Padding
     // tiles (rows >= n) are included: their products are zero, and the leader ignores them.
-    float xc[2], cacc[2] = {0.f, 0.f};
-    f4 xr[TT + 1];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int J = h ? TT - 1 - pr : pr;
-      const float v = in[16 * J + c];
-      xc[h] = (16 * J + c < n) ? v : 0.f;
+    float xc0, xc1;
+    f4 xr[TT];  // rows pr .. TT-1 (index I - pr)
+    {
+      const float v0 = in[16 * J0 + c], v1 = in[16 * J1 + c];
+      xc0 = (16 * J0 + c < n) ? v0 : 0.f;
+      xc1 = (16 * J1 + c < n) ? v1 : 0.f;
     }
 #pragma unroll
-    for (int l = 0; l <= TT; ++l) {
-      int I, J;
-      team_slot<NC, W>(w, j, l, I, J);
-      xr[l] = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
+    for (int r = 0; r < TT; ++r) {
+      const int I = min(pr + r, TT - 1);
+      xr[r] = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) xr[l][q] = (16 * I + 4 * g + q < n) ? xr[l][q] : 0.f;
+      for (int q = 0; q < 4; ++q) xr[r][q] = (16 * I + 4 * g + q < n) ? xr[r][q] : 0.f;
     }
-    pin(xc[0]);
-    pin(xc[1]);
+    pin(xc0);
+    pin(xc1);
 #pragma unroll
-    for (int l = 0; l <= TT; ++l) pin(xr[l]);
+    for (int r = 0; r < TT; ++r) pin(xr[r]);
+    float cacc0 = 0.f, cacc1 = 0.f;
 #pragma unroll
-    for (int l = 0; l <= TT; ++l) {
-      int I, J;
-      team_slot<NC, W>(w, j, l, I, J);
-      const bool h1 = !(l < TT - pr);
-      const f4 m = M[j * (TT + 1) + l];
-      const float xj = h1 ? xc[1] : xc[0];
+    for (int r = 0; r < TT; ++r) {
+      const int I = pr + r;
+      if (I >= TT) break;
+      const f4 m0 = M[j * (TT + 1) + r];  // tile (I, J0): slot I - pr
+      f4 racc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) racc[q] = m0[q] * xc0;
+      if (I > J0) {
+        float cp = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cp = fmaf(m0[q], xr[r][q], cp);
+        cacc0 += cp;
+      }
+      if (I >= J1) {  // tile (I, J1): slot I + 1
+        const f4 m1 = M[j * (TT + 1) + I + 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) racc[q] = fmaf(m1[q], xc1, racc[q]);
+        if (I > J1) {
+          float cp = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) cp = fmaf(m1[q], xr[r][q], cp);
+          cacc1 += cp;
+        }
+      }
       f4 rs;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rs[q] = row16_sum(m[q] * xj);
-      if (c == 0) *reinterpret_cast<f4*>(&ts.partR[J][16 * I + 4 * g]) = rs;
-      float cp = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) cp = fmaf(m[q], xr[l][q], cp);
-      cp = (J < I) ? cp : 0.f;  // the diagonal tile is stored in full: row sums only
-      if (h1) cacc[1] += cp; else cacc[0] += cp;
+      for (int q = 0; q < 4; ++q) rs[q] = row16_sum(racc[q]);
+      if (c == 0) *reinterpret_cast<f4*>(&ts.partR[pr][16 * I + 4 * g]) = rs;
     }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int J = h ? TT - 1 - pr : pr;
-      const float cs = col4_sum(cacc[h]);
-      if (g == 0) ts.partC[16 * J + c] = cs;
+    const float cs0 = col4_sum(cacc0), cs1 = col4_sum(cacc1);
+    if (g == 0) {
+      ts.partC[16 * J0 + c] = cs0;
+      ts.partC[16 * J1 + c] = cs1;
     }
   }
 }
 
-// leader side: out[p] = partC[p] + sum_{J <= p/16} partR[J][p] over the first TA chunks, 0 beyond
+// leader side: out[p] = partC[p] + sum_{pr <= p/16} partR[pr][p] over the first TA chunks, 0
+// beyond
 template <int NC, int W>
 __device__ __forceinline__ void team_symv_reduce(TeamSmem<NC, W>& ts, int n, float* out) {
-  constexpr int TT = NC / 16;
+  constexpr int NPAIR = NC / 32;
   const int lane = opaque_lane();
   n = uniform(n);
   const int TA = (n + 15) >> 4;
@@ -515,9 +573,9 @@ __device__ __forceinline__ void team_symv_reduce(TeamSmem<NC, W>& ts, int n, flo
     const int I = p >> 4;
     float acc = ts.partC[p];
 #pragma unroll
-    for (int J = 0; J < TT; ++J) {
-      const float v = ts.partR[J][p];
-      acc += (J <= I) ? v : 0.f;
+    for (int pr = 0; pr < NPAIR; ++pr) {
+      const float v = ts.partR[pr][p];
+      acc += (pr <= I) ? v : 0.f;
     }
     out[p] = (I < TA) ? acc : 0.f;
   }
