@@ -55,6 +55,7 @@ POLISH_REFINE = 4                                # SolverParams.polish_refine (d
 GLOBAL_BATCH = {1: 256, 2: 4096, 3: 65536}       # BASELINE.json configs[1..3]
 KERNEL_BINS = ((1, 0), (3, 2))                   # cmpc/_lib.py: kernel k serves these bins
 KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<192, 160>")
+TEAM_KERNEL_NAME = "solve_team_kernel<4>"  # B <= Plan.team_batch(): all bins, 4 waves per QP
 
 
 def algorithmic_flops(contact, iters, N=16):
@@ -204,6 +205,11 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
     """Roofline of the dominant solve kernel of the last timed steps: algorithmic bytes of the
     solves it processed / its average HIP-event duration (kernels run on their own streams)."""
     kern = kernel_of_bins(bins)
+    names = list(KERNEL_NAMES)
+    team = hasattr(plan.lib, "cmpc_plan_team_batch") and B_shard <= plan.team_batch()
+    if team:  # small batch: one team kernel (four waves per QP) serves every bin
+        kern = np.zeros_like(kern)
+        names[0] = TEAM_KERNEL_NAME
     avg = [ms[k] / max(calls[k], 1) for k in range(2)]
     q = int(np.argmax(avg))
     n_q = int(np.sum(kern == q))
@@ -212,15 +218,16 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
     fl_q = float(flops[kern == q].sum())
     tfs = fl_q / (avg[q] * 1e-3) / 1e12 if avg[q] > 0 else 0.0
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": KERNEL_NAMES[q],
-            "kernel_avg_ms": avg[q], "solves_per_launch": n_q, "bytes_per_solve": BYTES_PER_SOLVE,
-            "kernel_avg_ms_all": {KERNEL_NAMES[k]: avg[k] for k in range(2)},
-            "solves_per_kernel": {KERNEL_NAMES[k]: int(np.sum(kern == k)) for k in range(2)}}
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic if not team else None,
+            "kernel": names[q], "kernel_avg_ms": avg[q], "solves_per_launch": n_q,
+            "bytes_per_solve": BYTES_PER_SOLVE,
+            "kernel_avg_ms_all": {names[k]: avg[k] for k in range(2 - int(team))},
+            "solves_per_kernel": {names[k]: int(np.sum(kern == k)) for k in range(2 - int(team))}}
     comp = {"bound": "mfma", "achieved": tfs, "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
             "frac": tfs / F32_MATRIX_PEAK_TFS, "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
             "flops_per_solve": fl_q / max(n_q, 1)}
-    c = (counters or {}).get(KERNEL_NAMES[q].replace(", ", ","), None) or \
-        (counters or {}).get(KERNEL_NAMES[q], None)
+    c = None if team else ((counters or {}).get(KERNEL_NAMES[q].replace(", ", ","), None) or
+                           (counters or {}).get(KERNEL_NAMES[q], None))
     if c and c.get("SQ_INSTS_MFMA") and avg[q] > 0:
         # counted matrix work of this kernel per launch (PMC, profiles/) over its live duration
         ach = c["SQ_INSTS_MFMA"] * 2048.0 / (avg[q] * 1e-3) / 1e12

@@ -121,9 +121,16 @@ class Plan:
 
     def set_team(self, max_batch: int):
         """Small-batch (team) mode for solves of B <= max_batch: four waves per QP.
-        -1 = automatic (B <= 2 x CUs, the default), 0 = off (cmpc_plan_set_team)."""
+        -1 = automatic (B <= 4 x CUs, the default), 0 = off (cmpc_plan_set_team)."""
         _check(self.lib, self.lib.cmpc_plan_set_team(self._h, int(max_batch)),
                "cmpc_plan_set_team")
+
+    def team_batch(self) -> int:
+        """The largest batch solved in team mode (cmpc_plan_team_batch)."""
+        v = ctypes.c_int64()
+        _check(self.lib, self.lib.cmpc_plan_team_batch(self._h, ctypes.byref(v)),
+               "cmpc_plan_team_batch")
+        return int(v.value)
 
     def timing_read(self):
         """-> (ms_per_kernel[2], calls_per_kernel[2]) of the two solve kernels since the last

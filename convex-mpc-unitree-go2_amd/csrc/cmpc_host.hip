@@ -36,7 +36,7 @@ struct cmpc_plan {
   // (cmpc_team.hip), on the caller's stream
   int team_grid = 0;
   size_t team_slab = 0;
-  int64_t team_max_batch = -1;  // -1: automatic (two instances per CU at most)
+  int64_t team_max_batch = -1;  // -1: automatic (B <= 4 x CUs: at most one wave per SIMD)
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -309,6 +309,10 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
   return CMPC_OK;
 }
 
+static int64_t team_batch(const cmpc_plan* pl) {
+  return pl->team_max_batch >= 0 ? pl->team_max_batch : 4LL * pl->cus;
+}
+
 // team mode: one launch for every bin; timed as solve kernel 0 (kernel 1 records no call)
 static int record_team_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams& kp,
                               const cmpc::Inputs& in, const cmpc::Outputs& out, int64_t B) {
@@ -364,10 +368,10 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   cmpc::KParams kp = pl->kp;
   // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
-  // small batches: a team of kTeamWaves waves per QP (at most two instances per CU), all bins
-  // in one kernel on the caller's stream
-  const int64_t tmax = pl->team_max_batch >= 0 ? pl->team_max_batch : 2LL * pl->cus;
-  if (B <= tmax) return record_team_launch(pl, st, kp, in, out, B);
+  // small batches: a team of kTeamWaves waves per QP, all bins in one kernel on the caller's
+  // stream (measured faster than one wave per QP up to B = 4 x CUs on configs 1-3, slower from
+  // 2,048 up: DESIGN.md 4g)
+  if (B <= team_batch(pl)) return record_team_launch(pl, st, kp, in, out, B);
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
@@ -494,6 +498,12 @@ int cmpc_plan_set_team(cmpc_plan* pl, int64_t max_batch) {
   if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_team: null plan");
   if (max_batch < -1) return fail(CMPC_E_INVALID, "cmpc_plan_set_team: max_batch must be >= -1");
   pl->team_max_batch = max_batch;
+  return CMPC_OK;
+}
+
+int cmpc_plan_team_batch(const cmpc_plan* pl, int64_t* max_batch) {
+  if (!pl || !max_batch) return fail(CMPC_E_INVALID, "cmpc_plan_team_batch: null argument");
+  *max_batch = team_batch(pl);
   return CMPC_OK;
 }
 

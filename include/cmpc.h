@@ -239,9 +239,11 @@ int cmpc_plan_set_timing(cmpc_plan* plan, int enable);
 /* Small-batch mode.  A solve of B <= max_batch instances runs each QP on a workgroup of four
  * waves (one per SIMD of a CU) that split the condensation, the inversion and the matrix-vector
  * products, instead of one wave per QP: B = 256 on 256 CUs otherwise leaves 3 of every 4 SIMDs
- * idle.  Results are the same algorithm's (parity-tested in both modes).  max_batch = -1 (the
- * default) selects it automatically for B <= 2 x CUs; 0 disables it. */
+ * idle.  All four bins then run in one kernel on `stream` (timed as solve kernel 0).  Results
+ * are the same algorithm's (parity-tested in both modes).  max_batch = -1 (the default) selects
+ * it for B <= 4 x CUs; 0 disables it.  cmpc_plan_team_batch returns the effective bound. */
 int cmpc_plan_set_team(cmpc_plan* plan, int64_t max_batch);
+int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
 int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_kernel, int32_t* calls_per_kernel);
 
 /* Thread-local description of the last error returned on this thread ("" if none). */
