@@ -12,7 +12,7 @@ if [ "${FULL:-1}" = "1" ]; then
   timeout -k 10 500 python bench.py > gpurun_out/bench_full.json 2> gpurun_out/bench_full.err || { echo "bench failed"; tail gpurun_out/bench_full.err; exit 1; }
   cat gpurun_out/bench_full.json
 fi
-HEAD="--aux 0 --config ${CFG:-3}"
+HEAD="--aux 0 --config ${CFG:-3} ${BATCH:+--batch $BATCH}"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py $HEAD --steps 5 --warmup 1 > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -5 gpurun_out/prof.log; exit 1; }
 i=0
 pass() {

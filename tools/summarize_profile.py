@@ -45,6 +45,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tag", required=True)
     ap.add_argument("--root", default=str(REPO / "gpurun_out"))
+    ap.add_argument("--side", action="store_true",
+                    help="a side profile (not the headline): leave profiles/hbm_traffic.json and "
+                         "r02_counters.json alone")
     a = ap.parse_args()
     root = Path(a.root)
     out = REPO / "profiles"
@@ -56,7 +59,7 @@ def main():
     kern_ms = defaultdict(list)
     if trace.exists():
         rows = [r for r in csv.DictReader(open(trace)) if "solve_group_kernel" in r["Kernel_Name"]
-                or "bin_kernel" in r["Kernel_Name"]]
+                or "solve_team_kernel" in r["Kernel_Name"] or "bin_" in r["Kernel_Name"]]
         with open(out / f"{a.tag}_kernel_trace_solve.csv", "w", newline="") as fh:
             w = csv.writer(fh)
             w.writerow(["Kernel_Name", "Queue_Id", "Start_Timestamp", "End_Timestamp", "Duration_ms"])
@@ -71,7 +74,7 @@ def main():
     d = dispatches(root)
     per_kernel = defaultdict(lambda: defaultdict(list))
     for (p, _), r in d.items():
-        if "solve_group_kernel" not in r["kernel"]:
+        if "solve_group_kernel" not in r["kernel"] and "solve_team_kernel" not in r["kernel"]:
             continue
         name = r["kernel"].split("(")[0]
         for k, v in r.items():
@@ -98,7 +101,7 @@ def main():
                 s["mfma_frac_of_peak"] = s["mfma_tflops_at_trace_ms"] / PEAK_TFS
         summary[name] = s
     (out / f"{a.tag}_counters.json").write_text(json.dumps(summary, indent=1))
-    if a.tag != "r02":
+    if a.tag != "r02" and not a.side:
         (out / "r02_counters.json").write_text(json.dumps(summary, indent=1))
     # dominant kernel (longest median trace duration) -> the bench's traffic figure
     dom = max(summary, key=lambda n: summary[n].get("trace_ms_median", 0.0)) if summary else None
@@ -110,7 +113,8 @@ def main():
                "all_kernels": {n: s.get("hbm_bytes_per_launch") for n, s in summary.items()},
                "note": "per launch at the bench's headline batch (PMC, kernels serialised); fetch "
                        "doubled per the gfx950 FETCH_SIZE correction"}
-        (out / "hbm_traffic.json").write_text(json.dumps(res, indent=1))
+        if not a.side:
+            (out / "hbm_traffic.json").write_text(json.dumps(res, indent=1))
         (out / f"{a.tag}_hbm_traffic.json").write_text(json.dumps(res, indent=1))
     print(json.dumps(summary, indent=1))
 
