@@ -503,17 +503,21 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
   n = uniform(n);
 #pragma unroll
   for (int t = 0; t < C::NTL; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
-  float aA[4], aT[4], q2[4];  // A[c][4g + q] (A operand of A X), A[4g + q][c] (of A' X), Q2
+  // K = 12 state layout (as condense_tiles_fwd): accumulator position 4g + q holds state 3g + q
+  // for q < 3 and is padding for q = 3, so every product over the states is three MFMAs
+  const int sc = ((c & 3) < 3) ? 3 * (c >> 2) + (c & 3) : -1;
+  float aA[3], aT[3];  // A[sc][3g + q] (A operand of A X), A[3g + q][sc] (of A' X)
+  f4 q2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int r = 4 * g + q;
-    aA[q] = (c < 12 && r < 12) ? s.A[c * 12 + r] : 0.f;
-    aT[q] = (c < 12 && r < 12) ? s.A[r * 12 + c] : 0.f;
-    q2[q] = (r < 12 && r == c) ? s.Q2[r] : 0.f;
+  for (int q = 0; q < 3; ++q) {
+    const int r = 3 * g + q;
+    aA[q] = (sc >= 0) ? s.A[sc * 12 + r] : 0.f;
+    aT[q] = (sc >= 0) ? s.A[r * 12 + sc] : 0.f;
+    q2[q] = (r == sc) ? s.Q2[r] : 0.f;
   }
   float* Cs = s.G;  // C_i columns, param-major [p][12] (the G slab is free while condensing)
   // ---- backward: P_i and C_i = P_i B_i for i = N-1 .. 0 ----
-  f4 Pt = {q2[0], q2[1], q2[2], q2[3]};  // P_{N-1} = Q2 (diagonal)
+  f4 Pt = q2;  // P_{N-1} = Q2 (diagonal)
   WSYNC();
   for (int i = N - 1; i >= 0; --i) {
     const int p0 = s.off[i], p1 = s.off[i + 1];
@@ -521,19 +525,23 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
     for (int J = 0; J < C::TT; ++J) {
       if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform: chunks holding step i's params
       const int p = 16 * J + c;
-      f4 bt = {0.f, 0.f, 0.f, 0.f};
-      if (g < 3 && p < n) bt = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+      float bt[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bt[q] = (p < n) ? s.Bt[p * 12 + 3 * g + q] : 0.f;
       f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) d = mfma4(Pt[q], bt[q], d);  // C = P B (P symmetric)
-      if (g < 3 && p >= p0 && p < p1) *reinterpret_cast<f4*>(&Cs[p * 12 + 4 * g]) = d;
+      for (int q = 0; q < 3; ++q) d = mfma4(Pt[q], bt[q], d);  // C = P B (P symmetric)
+      if (p >= p0 && p < p1) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) Cs[p * 12 + 3 * g + q] = d[q];
+      }
     }
     if (i > 0) {  // P_{i-1} = Q2 + A' P_i A
       f4 y = {0.f, 0.f, 0.f, 0.f}, z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) y = mfma4(Pt[q], aT[q], y);   // Y = P A
+      for (int q = 0; q < 3; ++q) y = mfma4(Pt[q], aT[q], y);   // Y = P A
 #pragma unroll
-      for (int q = 0; q < 4; ++q) z = mfma4(aT[q], y[q], z);    // Z = A' Y
+      for (int q = 0; q < 3; ++q) z = mfma4(aT[q], y[q], z);    // Z = A' Y
 #pragma unroll
       for (int q = 0; q < 4; ++q) Pt[q] = z[q] + q2[q];
     }
@@ -553,7 +561,7 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
         if (kI[J] >= t) continue;  // uniform
         f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) d = mfma4(aA[q], Gd[J][q], d);
+        for (int q = 0; q < 3; ++q) d = mfma4(aA[q], Gd[J][q], d);
         Gd[J] = d;
       }
     }
@@ -562,19 +570,25 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
     for (int J = 0; J < C::TT; ++J) {
       if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
       const int p = 16 * J + c;
-      if (p >= p0 && p < p1 && g < 3) Gd[J] = *reinterpret_cast<const f4*>(&s.Bt[p * 12 + 4 * g]);
+      if (p >= p0 && p < p1) {
+        const float* bp = &s.Bt[p * 12 + 3 * g];
+        Gd[J] = f4{bp[0], bp[1], bp[2], 0.f};
+      }
     }
 #pragma unroll
     for (int I = 0; I < C::TT; ++I) {
       if (16 * I + 15 < p0 || 16 * I >= p1) continue;  // uniform: tile rows holding step t
       const int p = 16 * I + c;
-      f4 a = {0.f, 0.f, 0.f, 0.f};
-      if (p >= p0 && p < p1 && g < 3) a = *reinterpret_cast<const f4*>(&Cs[p * 12 + 4 * g]);
+      float a[3] = {0.f, 0.f, 0.f};
+      if (p >= p0 && p < p1) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[q] = Cs[p * 12 + 3 * g + q];
+      }
 #pragma unroll
       for (int J = 0; J <= I; ++J) {
         f4 acc = M[tile_index(I, J)];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc = mfma4(a[q], Gd[J][q], acc);
+        for (int q = 0; q < 3; ++q) acc = mfma4(a[q], Gd[J][q], acc);
         M[tile_index(I, J)] = acc;
       }
     }
@@ -626,8 +640,11 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
 template <int NC>
 __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
                                                f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
+#ifndef CMPC_BC_ALWAYS
+#define CMPC_BC_ALWAYS 0
+#endif
   if constexpr (NC <= 128) {  // the 1-wave-per-SIMD bins would spill the second form
-    if (P.latency_mode) {      // uniform
+    if (CMPC_BC_ALWAYS || P.latency_mode) {  // uniform
       condense_tiles_bc<NC>(s, P, M, n, shift);
       return;
     }

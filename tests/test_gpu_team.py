@@ -143,3 +143,15 @@ def test_team_park_restore_paths(team_plan):
     assert np.all(st == 1)
     err = rel_err_U(w, np.repeat(fx["w"], reps, axis=0))
     assert err.max() <= TOL_U, (err.max(), int(err.argmax()) // reps)
+
+
+@pytest.mark.parametrize("name", ["qp_cfg1.npz", "qp_cfg2.npz", "qp_nc192.npz"])
+def test_one_wave_latency_mode_parity(wave_plan, name):
+    """With team mode off, small batches run one wave per QP in latency mode (block-row
+    condensation for NC <= 128): same parity bar."""
+    from cmpc import solve_batch
+    fx = load_fixture(name)
+    w, st, it = solve_batch(fixture_batch(fx), plan=wave_plan)
+    assert np.all(st == 1), (st, it)
+    err = rel_err_U(w, fx["w"])
+    assert err.max() <= TOL_U, (err.max(), int(err.argmax()))
