@@ -83,13 +83,29 @@ int group_first_bin(int k) { return k == 0 ? 1 : 3; }
 
 constexpr int kTeamWaves = 4;
 
+// Elastic workgroups (cmpc_wave.hip solve_elastic_kernel: kEW waves, each its own instances,
+// the batch tail in team mode) or one wave per workgroup (solve_group_kernel).
+#ifndef CMPC_ELASTIC
+#define CMPC_ELASTIC 0
+#endif
+constexpr int kGroupWaves = CMPC_ELASTIC ? cmpc::kEW : 1;
+
 KernelFn group_fn(int k) {
+  if (CMPC_ELASTIC)
+    return k == 0 ? cmpc::solve_elastic_kernel<128, 96> : cmpc::solve_elastic_kernel<192, 160>;
   return k == 0 ? cmpc::solve_group_kernel<128, 96> : cmpc::solve_group_kernel<192, 160>;
 }
 
+// park slab per wave (floats): the one-wave inverse, or (elastic) a whole team's slots
+template <int NC>
+constexpr size_t wave_slab() {
+  return CMPC_ELASTIC ? std::max(cmpc::Cfg<NC>::SLAB, cmpc::TeamCfg<NC, cmpc::kEW>::SLAB)
+                      : cmpc::Cfg<NC>::SLAB;
+}
+
 size_t group_slab(int k) {
-  return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
-                : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
+  return k == 0 ? std::max(wave_slab<128>(), wave_slab<96>())
+                : std::max(wave_slab<192>(), wave_slab<160>());
 }
 }  // namespace
 
@@ -175,7 +191,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   size_t work_floats = 0;
   for (int k = 0; k < kNumGroups; ++k) {
     int nb = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64 * kGroupWaves, 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
 #ifdef CMPC_STAMPS
@@ -187,7 +203,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     pl->grid[k] = nb * cus;
     pl->slab[k] = group_slab(k);
     pl->work_off[k] = work_floats;
-    work_floats += (size_t)pl->grid[k] * pl->slab[k];
+    work_floats += (size_t)pl->grid[k] * kGroupWaves * pl->slab[k];
   }
   {
     int nb = 0;
@@ -295,7 +311,7 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64), 0, s, kp, in, out,
+  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64 * kGroupWaves), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
@@ -375,6 +391,30 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
+#ifndef CMPC_CLASS_ORDER
+#define CMPC_CLASS_ORDER 0
+#endif
+  if (CMPC_CLASS_ORDER == 1 && big) {  // heavy class on the caller's stream, light one forked after
+    if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+    rc = record_launch(pl, 1, st, kp, in, out, g1);
+    if (rc != CMPC_OK) return rc;
+    if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
+      return hip_fail(e, "hipStreamWaitEvent");
+    const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
+    rc = record_launch(pl, 0, pl->side, kp, in, out, g0);
+    if (rc != CMPC_OK) return rc;
+    if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
+    return CMPC_OK;
+  }
+  if (CMPC_CLASS_ORDER == 2 && big) {  // serialised: heavy class, then light class
+    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+    rc = record_launch(pl, 1, st, kp, in, out, g1);
+    if (rc != CMPC_OK) return rc;
+    const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
+    return record_launch(pl, 0, st, kp, in, out, g0);
+  }
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)

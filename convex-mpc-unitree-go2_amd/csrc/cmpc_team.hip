@@ -625,15 +625,18 @@ __device__ __forceinline__ void team_issue(TeamSmem<NC, W>& ts, int& seq, int op
 }
 
 // helpers: execute the leader's commands until kOpExit (one bin's drain loop)
+// (started: the barrier of the first command has been passed already -- elastic teams)
 template <int NC, int W, int WV>
 __device__ __forceinline__ void team_helper(Smem<NC>& s, TeamSmem<NC, W>& ts, const KParams& P,
-                                            float* __restrict__ park, int& seq) {
+                                            float* __restrict__ park, int& seq,
+                                            bool started = false) {
   constexpr int w = WV;
   f4 M[TeamCfg<NC, W>::SLOTS];
 #pragma unroll
   for (int t = 0; t < TeamCfg<NC, W>::SLOTS; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
   for (;;) {
-    team_barrier();
+    if (!started) team_barrier();
+    started = false;
     const int* cm = ts.cmd[seq & 1];
     const int op = uniform(cm[0]), a0 = uniform(cm[1]), a1 = uniform(cm[2]);
     ++seq;

@@ -185,7 +185,9 @@ struct Cfg {
   static constexpr int TT = NC / 16;             // 16x16 tile rows
   static constexpr int NTL = TT * (TT + 1) / 2;  // lower-triangle tiles (f4 per lane each)
   static constexpr int THREADS = 64;             // one wave per QP
-  static constexpr int SLAB = NTL * 256;         // per wave: park slab of the inverse (floats)
+  // per wave (floats): park slab of the inverse, then the ADMM state (x, z, y) kept aside
+  // during the interior-point fallback (ipm_save)
+  static constexpr int SLAB = NTL * 256 + 3 * NC;
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
   static constexpr int WPE = CMPC_WPE_OVERRIDE;
 };
@@ -210,6 +212,10 @@ constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least thi
 constexpr int kBackoffCap = 3;       // polish back-off doubles per failed session, up to 8x
 constexpr int kLateRepairs = 3;      // repair budget of the sessions after two failed ones
 constexpr int kFailMem = 4;
+#ifndef CMPC_SEEN_MAX
+#define CMPC_SEEN_MAX 1000  // (A/B: 2 resumes repairs after two remembered-set sessions in a row)
+#endif
+constexpr int kSeenMax = CMPC_SEEN_MAX;  // sessions in a row from remembered sets before repairs resume
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
 
@@ -1287,13 +1293,315 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 #include "cmpc_team.hip"  // W waves per QP for small batches (leader + helpers)
 
 // ------------------------------------------------------------------------------------------
+// Interior-point identification of the face set, for hard instances.  A few instances per
+// thousand keep ADMM's face set "stable" but wrong for a long time: their polish sessions fail,
+// repair, fail again, and the instance runs 100-200 ADMM iterations and 20-45 factorizations
+// (5-10 M cycles), which sets the time of any batch or shard that holds one.  After kIpmAfter
+// failed sessions such an instance runs kIpmIters Mehrotra predictor-corrector steps on the
+// condensed QP
+//     min 1/2 u'Pu + q'u   s.t.  G_t u_t <= h_t per stance triple (the 5 pyramid rows),
+// keeping the slacks s = h - G u exact (u stays strictly inside K) and solving each Newton
+// system (P + G' diag(z/s) G) du = rhs with the fp32 inverse of that matrix (P parked once, the
+// 3x3 barrier block of every triple added to the tiles, the 4-pivot sweep).  Its face set (rows
+// with multiplier z > slack s) then starts a polish session with the full repair budget.
+// Prototyped in NumPy on the slowest config-3 instances: after 11 fp32 steps the polish +
+// repairs need 1-5 factorizations (ADMM had needed 20-45).
+// ------------------------------------------------------------------------------------------
+#ifndef CMPC_IPM_AFTER
+#define CMPC_IPM_AFTER 0  // failed polish sessions before the interior-point fallback (0: never)
+#endif
+constexpr int kIpmAfter = CMPC_IPM_AFTER;
+constexpr int kIpmIters = 11;
+
+__device__ __forceinline__ float wave_sum(float v) { return col4_sum(row16_sum(v)); }
+__device__ __forceinline__ float wave_min(float v) { return -wave_max(-v); }
+
+// tiles += G' diag(d) G: the 3x3 block of each triple (d = z / s of its 5 rows at
+// dd[i * ntri + t]); only the diagonal tiles and the one below each can hold such entries
+template <int NC>
+__device__ __forceinline__ void ipm_add_barrier(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL], int n,
+                                                int ntri, float mu, const float* dd) {
+  using C = Cfg<NC>;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  WSYNC();
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+#pragma unroll
+    for (int J = (I > 0 ? I - 1 : 0); J <= I; ++J) {
+      f4 m = M[tile_index(I, J)];
+      const int col = 16 * J + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        const int t = row / 3;
+        if (row < n && col < n && col / 3 == t) {
+          const int a = row - 3 * t, b = col - 3 * t;
+          const float d0 = dd[t], d1 = dd[ntri + t], d2 = dd[2 * ntri + t], d3 = dd[3 * ntri + t],
+                      d4 = dd[4 * ntri + t];
+          float w;
+          if (a == 2 && b == 2) w = d0 + mu * mu * (d1 + d2 + d3 + d4);
+          else if (a == 0 && b == 0) w = d1 + d2;
+          else if (a == 1 && b == 1) w = d3 + d4;
+          else if (a + b == 2) w = -mu * (d1 - d2);  // (x, z)
+          else if (a + b == 3) w = -mu * (d3 - d4);  // (y, z)
+          else w = 0.f;                              // (x, y)
+          m[q] += w;
+        }
+      }
+      M[tile_index(I, J)] = m;
+    }
+  }
+}
+
+// Rows of a triple u = (fx, fy, fz): G u <= h with
+//   r0: -fz <= -fz_min,  r1: fx - mu fz <= 0,  r2: -fx - mu fz <= 0,  r3/r4: the same for fy.
+__device__ __forceinline__ void ipm_rows(float ux, float uy, float uz, float mu, float fzm,
+                                         float (&g)[5]) {  // G u - h: minus the slacks
+  g[0] = fzm - uz;
+  g[1] = ux - mu * uz;
+  g[2] = -ux - mu * uz;
+  g[3] = uy - mu * uz;
+  g[4] = -uy - mu * uz;
+}
+__device__ __forceinline__ void ipm_gdir(float dx, float dy, float dz, float mu, float (&g)[5]) {
+  g[0] = -dz;
+  g[1] = dx - mu * dz;
+  g[2] = -dx - mu * dz;
+  g[3] = dy - mu * dz;
+  g[4] = -dy - mu * dz;
+}
+
+// largest step a in (0, 1] keeping v + a dv > 0, lane-local
+__device__ __forceinline__ float ipm_maxstep(const float (&v)[5], const float (&dv)[5]) {
+  float a = 1.f;
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+    if (dv[i] < 0.f) a = fminf(a, -v[i] / dv[i]);
+  return a;
+}
+
+// Leaves the face set in s.code (lane t = triple t), u in s.x and s.z, the multiplier
+// y = G' z in s.y; clobbers the park slab (the ADMM inverse is no longer parked) and M.
+template <int NC>
+__device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
+                                             f4 (&M)[Cfg<NC>::NTL], float* __restrict__ park,
+                                             int n, int ntri, bool tr = false) {
+  static_assert(offsetof(Smem<NC>, v) == offsetof(Smem<NC>, y) + NC * sizeof(float),
+                "y and v are one free 2 NC block during the interior-point steps");
+  const float mu = P.mu, fzm = P.fz_min;
+  n = uniform(n);
+  ntri = uniform(ntri);
+  condense_tiles<NC>(s, P, M, n, uniformf(P.sigma));  // P (+ sigma), parked for every step
+  park_store<NC>(park, M);
+  float* dd = s.y;  // z / s of row i of triple t at dd[i * ntri + t] (5 ntri <= 2 NC floats)
+  // multipliers and slacks of this lane's triple.  The slacks are their own variables, moved
+  // by the same steps as u (s + G u = h holds to rounding): recomputing h - G u would cancel
+  // a small slack of an active row to nothing in fp32 (measured on the NumPy transcription:
+  // non-finite steps and wrong face sets).
+  float zc[5], sl[5];
+  {
+    const int l = opaque_lane();
+    WSYNC();
+    if (l < ntri) {  // interior start: (0, 0, 2 fz_min), all multipliers 1
+      s.x[3 * l] = 0.f;
+      s.x[3 * l + 1] = 0.f;
+      s.x[3 * l + 2] = 2.f * fzm;
+    }
+    float gu[5];
+    ipm_rows(0.f, 0.f, 2.f * fzm, mu, fzm, gu);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      zc[i] = (l < ntri) ? 1.f : 0.f;
+      sl[i] = (l < ntri) ? -gu[i] : 1.f;
+    }
+  }
+  const float m_inv = 1.f / (5.f * (float)max(ntri, 1));
+  for (int it = 0; it < kIpmIters; ++it) {
+    gradient<NC>(s, P, n, s.x, s.g);  // grad f(u)
+    const int l = opaque_lane();
+    const bool own = l < ntri;
+    WSYNC();
+    float sz = 0.f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      sz += sl[i] * zc[i];
+      if (own) dd[i * ntri + l] = zc[i] / sl[i];
+    }
+    const float mu_c = wave_sum(sz) * m_inv;
+    park_load<NC>(park, M);
+    ipm_add_barrier<NC>(s, M, n, ntri, mu, dd);
+    invert_tiles<NC>(s, M, n);
+    // predictor: rhs = -grad f (the slacks are exact, so the primal residual is zero)
+    for (int p = l; p < n; p += 64) s.r[p] = -s.g[p];
+    symv<NC>(s, M, n, s.r, s.dl);
+    float dsa[5], dza[5];
+    {
+      WSYNC();
+      float gd[5];
+      ipm_gdir(own ? s.dl[3 * l] : 0.f, own ? s.dl[3 * l + 1] : 0.f, own ? s.dl[3 * l + 2] : 0.f,
+               mu, gd);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        dsa[i] = own ? -gd[i] : 0.f;
+        dza[i] = own ? -zc[i] - zc[i] * dsa[i] / sl[i] : 0.f;
+      }
+    }
+    const float apa = wave_min(ipm_maxstep(sl, dsa)), ada = wave_min(ipm_maxstep(zc, dza));
+    float sza = 0.f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) sza += (sl[i] + apa * dsa[i]) * (zc[i] + ada * dza[i]);
+    const float mu_a = wave_sum(own ? sza : 0.f) * m_inv;
+    const float rat = mu_a / fmaxf(mu_c, 1e-30f);
+    const float smu = rat * rat * rat * mu_c;  // sigma mu (Mehrotra's centring)
+    // corrector: rhs = -grad f + G' ((dsa dza - sigma mu) / s)
+    float wv[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) wv[i] = (dsa[i] * dza[i] - smu) / sl[i];
+    WSYNC();
+    if (own) {
+      s.r[3 * l] = -s.g[3 * l] + (wv[1] - wv[2]);
+      s.r[3 * l + 1] = -s.g[3 * l + 1] + (wv[3] - wv[4]);
+      s.r[3 * l + 2] = -s.g[3 * l + 2] - wv[0] - mu * (wv[1] + wv[2] + wv[3] + wv[4]);
+    }
+    symv<NC>(s, M, n, s.r, s.dl);
+    float du[3], ds[5], dz[5];
+    {
+      WSYNC();
+#pragma unroll
+      for (int a = 0; a < 3; ++a) du[a] = own ? s.dl[3 * l + a] : 0.f;
+      float gd[5];
+      ipm_gdir(du[0], du[1], du[2], mu, gd);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        ds[i] = own ? -gd[i] : 0.f;
+        const float rc = sl[i] * zc[i] + dsa[i] * dza[i] - smu;
+        dz[i] = own ? (-zc[i] * ds[i] - rc) / sl[i] : 0.f;
+      }
+    }
+    const float ap = 0.99f * wave_min(ipm_maxstep(sl, ds)), ad = 0.99f * wave_min(ipm_maxstep(zc, dz));
+#ifdef CMPC_TRACE
+    if (tr && l == 0)
+      printf("  ipm %d mu %g mu_aff %g steps aff %g %g steps %g %g\n", it, mu_c, mu_a, apa, ada, ap, ad);
+#endif
+    // a collapsed step is fp32 running out near the end: keep the last iterate
+    if (it > 0 && ap < 0.1f) break;
+    WSYNC();
+    if (own) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) s.x[3 * l + a] += ap * du[a];
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      zc[i] += ad * dz[i];
+      sl[i] += ap * ds[i];
+    }
+  }
+  // the face set (rows whose multiplier exceeds their slack), the point and its multiplier
+  const int l = opaque_lane();
+  WSYNC();
+  bool bad = false;
+  if (l < ntri) {
+    const float ux = s.x[3 * l], uy = s.x[3 * l + 1], uz = s.x[3 * l + 2];
+    bool act[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) act[i] = zc[i] > sl[i];
+    int code = act[0] ? 1 : 0;
+    if (act[1] && (!act[2] || zc[1] >= zc[2])) code |= 2;
+    else if (act[2]) code |= 4;
+    if (act[3] && (!act[4] || zc[3] >= zc[4])) code |= 8;
+    else if (act[4]) code |= 16;
+    s.code[l] = code;
+    s.z[3 * l] = ux;
+    s.z[3 * l + 1] = uy;
+    s.z[3 * l + 2] = uz;
+    s.y[3 * l] = zc[1] - zc[2];  // y = G' z (the ADMM dual at a KKT point)
+    s.y[3 * l + 1] = zc[3] - zc[4];
+    s.y[3 * l + 2] = -zc[0] - mu * (zc[1] + zc[2] + zc[3] + zc[4]);
+    bad = !(isfinite(ux) && isfinite(uy) && isfinite(uz) && isfinite(s.y[3 * l]) &&
+            isfinite(s.y[3 * l + 1]) && isfinite(s.y[3 * l + 2]));
+#ifdef CMPC_TRACE
+    if (tr) printf("  ipm lane %d code %d z %g %g %g %g %g s %g %g %g %g %g\n", l, s.code[l], zc[0], zc[1],
+                   zc[2], zc[3], zc[4], sl[0], sl[1], sl[2], sl[3], sl[4]);
+#endif
+  }
+  WSYNC();
+  return __any(bad) == 0;
+}
+
+// the ADMM state (x, z, y) kept aside in the tail of the wave's park slab while the
+// interior-point steps and their polish session run; restored exactly if that session fails
+// (restoring only z and y -- x = z -- left a large dual residual, and the next adaptive-rho
+// update then dropped rho 10x: one hard instance crawled to max_iter)
+template <int NC>
+__device__ __forceinline__ void ipm_save(Smem<NC>& s, float* __restrict__ keep, int n) {
+  WSYNC();
+  for (int p = opaque_lane(); p < n; p += 64) {
+    keep[p] = s.x[p];
+    keep[NC + p] = s.z[p];
+    keep[2 * NC + p] = s.y[p];
+  }
+}
+template <int NC>
+__device__ __forceinline__ void ipm_restore(Smem<NC>& s, const float* __restrict__ keep, int n) {
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
+  for (int p = opaque_lane(); p < n; p += 64) {
+    const float xv = keep[p], zv = keep[NC + p], yv = keep[2 * NC + p];
+    s.x[p] = xv;
+    s.z[p] = zv;
+    s.y[p] = yv;
+  }
+  WSYNC();
+}
+
+// ------------------------------------------------------------------------------------------
+// Elastic teams (large batches, solve_elastic_kernel).  The persistent kernel's workgroup is
+// kEW waves, one per SIMD of a CU, each draining the bin queues with instances of its own (one
+// wave per QP, the whole lower triangle in its registers).  A wave that finds the queues empty
+// goes idle at the workgroup barrier.  When every other wave of the workgroup is idle, the last
+// running wave turns them into helpers at its next factorization: from then on its instance runs
+// in team mode (cmpc_team.hip: tiles split over kEW waves, the idle waves' instance images hold
+// the team block).  The batch tail -- the few slow instances that set the time of a small shard
+// -- then runs on four SIMDs instead of one.
+// ------------------------------------------------------------------------------------------
+constexpr int kEW = 4;
+
+struct ElasticCtl {
+  int idle;    // waves of the workgroup with no instance left
+  int leader;  // wave index of the team's leader (-1: no team; the waiting waves exit)
+  int nc;      // bin capacity of the leader's instance
+};
+
+struct Elastic {
+  ElasticCtl* ctl;
+  unsigned char* raw;  // the workgroup's instance images, `region` bytes per wave
+  int region;
+  int wv;              // this wave's index in the workgroup
+  int* seq;            // this wave's team command sequence (team_issue)
+  bool* team;          // this wave leads a team
+};
+
+// the team block of leader L lives in the image of wave L + 1 (idle once the team forms)
+template <int NC>
+__device__ __forceinline__ TeamSmem<NC, kEW>* elastic_team_block(const Elastic* el, int L) {
+  return reinterpret_cast<TeamSmem<NC, kEW>*>(el->raw + ((L + 1) & (kEW - 1)) * el->region);
+}
+
+// the first SLOTS tiles of a one-wave register array, as the team layout's slot array
+template <int NC>
+__device__ __forceinline__ f4 (&team_slots(f4 (&M)[Cfg<NC>::NTL]))[TeamCfg<NC, kEW>::SLOTS] {
+  static_assert(TeamCfg<NC, kEW>::SLOTS <= Cfg<NC>::NTL, "team slots fit the one-wave array");
+  return *reinterpret_cast<f4(*)[TeamCfg<NC, kEW>::SLOTS]>(&M[0]);
+}
+
+// ------------------------------------------------------------------------------------------
 // one QP instance on one wave (W = 1) or led by wave 0 of a W-wave team (cmpc_team.hip)
 // A polish session starts from the face set in s.code: record it as the session's first tried
 // set and look it up among the starting sets of failed sessions.  Returns the session's repair
 // budget (none for a remembered set).
 template <int NC>
 __device__ __forceinline__ int session_start(Smem<NC>& s, const KParams& P, int ntri, int nfail,
-                                             int& ntried, bool& seen) {
+                                             int& ntried, bool& seen, int& nseen) {
   const int l = opaque_lane();
   WSYNC();
   uint8_t c = 0;
@@ -1309,7 +1617,14 @@ __device__ __forceinline__ int session_start(Smem<NC>& s, const KParams& P, int 
     const bool diff = (l < ntri) && (s.fpat[k][l] != c);
     seen |= (__any(diff) == 0);
   }
-  if (seen) return 0;
+  // A remembered set is polished once more without repairs -- but not forever: ADMM can settle
+  // on a remembered set (its true face set, where the polish fails only in fp32), and after
+  // kSeenMax such sessions in a row the set gets repairs again (as a new failed session)
+  if (seen) {
+    if (++nseen <= kSeenMax) return 0;
+    seen = false;
+  }
+  nseen = 0;
   // after two failed sessions the repair budget shrinks: a wandering repair sequence costs a
   // factorization per step (cfg1 +1 %, cfg2 +1-2 %)
   return (nfail >= 2) ? min(P.polish_repairs, kLateRepairs) : P.polish_repairs;
@@ -1334,9 +1649,14 @@ template <int NC, int W>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
                                                float* __restrict__ park, TeamSmem<NC, W>* ts,
-                                               int* seq) {
+                                               int* seq, const Elastic* el = nullptr) {
   // W = 1: the whole lower triangle in this wave's registers; W > 1: this wave's team slots
   f4 M[TeamCfg<NC, W>::SLOTS];
+  // W = 1 in an elastic workgroup: this instance switches to team mode (the idle waves of the
+  // workgroup as helpers) at a factorization once every other wave is idle; from then on the
+  // matrix lives in the team's slots (the first SLOTS entries of M here)
+  bool eteam = false;
+  TeamSmem<NC, kEW>* ets = nullptr;
   static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
   const int lane = opaque_lane();
   const int N = P.N;
@@ -1470,6 +1790,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int dg_fact = 0, dg_pol = 0;
   const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
 #endif
+#ifdef CMPC_DIAG_TIMES  // diagnostic build: start / end on the 100 MHz constant clock
+  const unsigned long long dt_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   bool polished = false;
   float rp = 0.f, rd = 0.f, np_ = 0.f, nd = 0.f;
   int stable = 0;
@@ -1484,6 +1807,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int ntried = 0;         // face sets tried in the current session
   bool seen_start = false;  // the current session started from a remembered failed set
   int last_pol = 0;       // iteration of the last polish session
+  bool ipm_done = false;  // the interior-point fallback ran (at most once per instance)
+  int nsfail = 0;         // failed sessions, remembered starts included
+  int nseen = 0;          // sessions in a row that started from a remembered set
+  bool ipm_session = false;  // the current polish session started from its face set
   const float alpha = P.alpha;
   if (n == 0) status = 1;
   if (n > 0 && in.w_init != nullptr) {
@@ -1492,7 +1819,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     // repairs fail, ADMM starts from the warm (x, z, y) as above
     WSYNC();
     if (lane < ntri) s.code[lane] = s.pcode[lane];
-    repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
+    repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start, nseen);
     nact = polish_setup<NC>(s, P, Bg, ntri);
     shift = P.sigma;
     in_polish = true;
@@ -1504,12 +1831,33 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       ++dg_fact;
 #endif
       if constexpr (W == 1) {
-        CMPC_T0(t_c);
-        condense_tiles<NC>(s, P, M, nact, uniformf(shift));
-        CMPC_ACC(0, t_c);
-        CMPC_T0(t_i);
-        invert_tiles<NC>(s, M, nact);
-        CMPC_ACC(1, t_i);
+        if (el != nullptr && !eteam) {
+          const int idle = uniform(*reinterpret_cast<volatile int*>(&el->ctl->idle));
+          if (idle == kEW - 1) {  // every other wave is idle: they become this instance's team
+            eteam = true;
+            parked = false;  // a parked inverse has the one-wave layout: refactor instead
+            ets = elastic_team_block<NC>(el, el->wv);
+            WSYNC();
+            if (lane == 0) {
+              el->ctl->leader = el->wv;
+              el->ctl->nc = NC;
+            }
+            *el->seq = 0;
+            *el->team = true;
+          }
+        }
+        if (eteam) {
+          CMPC_T0(t_c);
+          team_factor_lead<NC, kEW>(s, *ets, *el->seq, P, team_slots<NC>(M), nact, uniformf(shift));
+          CMPC_ACC(0, t_c);
+        } else {
+          CMPC_T0(t_c);
+          condense_tiles<NC>(s, P, M, nact, uniformf(shift));
+          CMPC_ACC(0, t_c);
+          CMPC_T0(t_i);
+          invert_tiles<NC>(s, M, nact);
+          CMPC_ACC(1, t_i);
+        }
       } else {
         CMPC_T0(t_c);
         team_factor_lead<NC, W>(s, *ts, *seq, P, M, nact, uniformf(shift));
@@ -1525,8 +1873,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       float step = 3.0e38f, prev = 3.0e38f;
       for (int q = 0; q < CMPC_REFINE_N + kRefineExtra; ++q) {
         gradient<NC, (W > 1)>(s, P, nact, s.v, s.g, pwc, twc);
-        if constexpr (W == 1) symv<NC>(s, M, nact, s.g, s.dl);
-        else team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
+        if constexpr (W == 1) {
+          if (eteam) team_symv_lead<NC, kEW>(s, *ets, *el->seq, team_slots<NC>(M), nact, s.g, s.dl);
+          else symv<NC>(s, M, nact, s.g, s.dl);
+        } else {
+          team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
+        }
         float m = 0.f, mv = 1.f;
         for (int p = lane; p < nact; p += 64) {
           const float vn = s.v[p] - s.dl[p];
@@ -1582,6 +1934,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         break;
       }
       // the session failed: remember its starting face set (unless it came from the memory)
+      ++nsfail;
       if (!seen_start) {
         const int l = opaque_lane();
         if (l < ntri) s.fpat[nfail % kFailMem][l] = s.tpat[0][l];
@@ -1591,6 +1944,42 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       build_admm_basis<NC>(s, P, Bg, ntri);
       in_polish = false;
       nact = n;
+      if (ipm_session) {  // ADMM resumes from where it was before the interior-point steps
+        ipm_session = false;
+        ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
+      }
+      if constexpr (W == 1 && kIpmAfter > 0) {
+        if (!eteam && !ipm_done && nsfail >= kIpmAfter) {
+          // a hard instance: identify the face set by interior-point steps, then polish it
+          // with the full repair budget (ADMM resumes where it was if that session fails too)
+          ipm_done = true;
+          float* keep = park + Cfg<NC>::NTL * 256;
+          ipm_save<NC>(s, keep, n);
+#ifdef CMPC_TRACE
+          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri, b == CMPC_TRACE);
+#else
+          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri);
+#endif
+          parked = false;
+          if (!ok_ipm) {  // (non-finite steps) back to ADMM as it was, refactoring first
+            ipm_restore<NC>(s, keep, n);
+            refactor = true;
+            shift = uniformf(P.sigma + rho);
+            continue;
+          }
+          ipm_session = true;
+          session_start<NC>(s, P, ntri, nfail, ntried, seen_start, nseen);
+          seen_start = false;
+          repairs_left = P.polish_repairs;
+          nact = polish_setup<NC>(s, P, Bg, ntri);
+          shift = P.sigma;
+          refactor = true;
+          in_polish = true;
+          last_pol = it;
+          stable = -(P.polish_stable << min(nfail, kBackoffCap));
+          continue;
+        }
+      }
       if (rho_low) {  // a hard instance: back to the standard rho0 (one refactor)
         rho_low = false;
         rho = uniformf(P.rho0);
@@ -1601,7 +1990,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       shift = uniformf(P.sigma + rho);
       if (parked) {
         if constexpr (W == 1) {
-          park_load<NC>(park, M);
+          if (eteam) {
+            team_issue<NC, kEW>(*ets, *el->seq, kOpParkLoad, 0, 0, 0);
+            team_park_load<NC, kEW, 0>(park, team_slots<NC>(M), 0);
+          } else {
+            park_load<NC>(park, M);
+          }
         } else {
           team_issue<NC, W>(*ts, *seq, kOpParkLoad, 0, 0, 0);
           team_park_load<NC, W, 0>(park, M, 0);
@@ -1626,8 +2020,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         }
       }
     }
-    if constexpr (W == 1) symv<NC>(s, M, n, s.r, s.dl);
-    else team_symv_lead<NC, W>(s, *ts, *seq, M, n, s.r, s.dl);
+    if constexpr (W == 1) {
+      if (eteam) team_symv_lead<NC, kEW>(s, *ets, *el->seq, team_slots<NC>(M), n, s.r, s.dl);
+      else symv<NC>(s, M, n, s.r, s.dl);
+    } else {
+      team_symv_lead<NC, W>(s, *ts, *seq, M, n, s.r, s.dl);
+    }
     CMPC_T0(t_rest);
     const bool last = (it == P.max_iter);
     const bool adapt = P.adaptive_interval > 0 && (it % P.adaptive_interval) == 0;
@@ -1713,7 +2111,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       parked = !refactor && !rho_low && nfail > 0;
       if (parked) {  // restored if the polish fails
         if constexpr (W == 1) {
-          park_store<NC>(park, M);
+          if (eteam) {
+            team_issue<NC, kEW>(*ets, *el->seq, kOpParkStore, 0, 0, 0);
+            team_park_store<NC, kEW, 0>(park, team_slots<NC>(M), 0);
+          } else {
+            park_store<NC>(park, M);
+          }
         } else {
           team_issue<NC, W>(*ts, *seq, kOpParkStore, 0, 0, 0);
           team_park_store<NC, W, 0>(park, M, 0);
@@ -1722,7 +2125,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #else
       parked = false;      // a failed polish refactors the ADMM matrix instead
 #endif
-      repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
+      repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start, nseen);
       nact = polish_setup<NC>(s, P, Bg, ntri);
       CMPC_ACC(14, t_ps);
       shift = P.sigma;
@@ -1820,9 +2223,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     }
   }
   if (lane == 0) {
-#ifdef CMPC_DIAG_COUNTS  // diagnostic build: iters | attempts | factorizations, cycles / 16
+#if defined(CMPC_DIAG_COUNTS)  // diagnostic build: iters | attempts | factorizations, cycles / 16
     out.status[b] = (int)((__builtin_amdgcn_s_memtime() - dg_t0) >> 4);
     out.iters[b] = iters + 1000 * dg_pol + 1000000 * dg_fact;
+#elif defined(CMPC_DIAG_TIMES)  // start (10 ns ticks, low 31 bits) | duration + 1e9 if teamed
+    out.status[b] = (int)(dt_t0 & 0x7fffffffull);
+    out.iters[b] = (int)(__builtin_amdgcn_s_memrealtime() - dt_t0) + (eteam ? 1000000000 : 0);
 #else
     out.status[b] = status;
     out.iters[b] = iters;
@@ -1840,7 +2246,7 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
                                           const Outputs& out, const int* __restrict__ list,
                                           const int* __restrict__ count, int* __restrict__ head,
                                           float* __restrict__ park, TeamSmem<NC, W>* ts = nullptr,
-                                          int* seq = nullptr) {
+                                          int* seq = nullptr, const Elastic* el = nullptr) {
   const int lane = opaque_lane();
   WSYNC();
   if (lane < 12) {  // KParams copies (each bin's Smem layout places them differently)
@@ -1853,7 +2259,7 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
     if (lane == 0) idx = atomicAdd(head, 1);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= total) break;
-    solve_instance<NC, W>(s, P, (int64_t)list[idx], in, out, park, ts, seq);
+    solve_instance<NC, W>(s, P, (int64_t)list[idx], in, out, park, ts, seq, el);
   }
   if constexpr (W > 1) team_issue<NC, W>(*ts, *seq, kOpExit, 0, 0, 0);
 }
@@ -1887,6 +2293,95 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
   WSYNC();
   if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
 #endif
+}
+
+// Elastic workgroup, after this wave's drain loops: a team leader releases its helpers (its
+// instance is done and the queues are empty, so every other wave is idle); any other wave goes
+// idle -- the last one to do so releases the waiting waves, the others wait at the workgroup
+// barrier for the first command of a team (or the release) and then serve as helpers.
+template <int NC>
+__device__ __forceinline__ void elastic_help(const Elastic& el, int L, const KParams& P,
+                                             float* __restrict__ lpark, int& seq) {
+  Smem<NC>& ls = *reinterpret_cast<Smem<NC>*>(el.raw + L * el.region);
+  TeamSmem<NC, kEW>& ts = *elastic_team_block<NC>(&el, L);
+  const int rel = (el.wv - L) & (kEW - 1);  // helper index within the team (the leader is 0)
+  if (rel == 1) team_helper<NC, kEW, 1>(ls, ts, P, lpark, seq, true);
+  else if (rel == 2) team_helper<NC, kEW, 2>(ls, ts, P, lpark, seq, true);
+  else team_helper<NC, kEW, 3>(ls, ts, P, lpark, seq, true);
+}
+
+template <int NCA, int NCB>
+__device__ __forceinline__ void elastic_finish(const Elastic& el, const KParams& P,
+                                               float* __restrict__ park0, size_t slab) {
+  const int lane = opaque_lane();
+  ElasticCtl& ctl = *el.ctl;
+  if (*el.team) {  // (uniform) the leader: release the team
+    if (uniform(ctl.nc) == NCA) team_issue<NCA, kEW>(*elastic_team_block<NCA>(&el, el.wv), *el.seq, kOpExit, 0, 0, 0);
+    else team_issue<NCB, kEW>(*elastic_team_block<NCB>(&el, el.wv), *el.seq, kOpExit, 0, 0, 0);
+    return;
+  }
+  WSYNC();
+  int old = 0;
+  if (lane == 0) old = atomicAdd(&ctl.idle, 1);
+  old = uniform(old);
+  if (old == kEW - 1) {  // the last wave with nothing to lead: release the waiting waves
+    if (lane == 0) ctl.leader = -1;
+    team_barrier();
+    return;
+  }
+  team_barrier();  // the first command of a team, or the release
+  const int L = uniform(*reinterpret_cast<volatile int*>(&ctl.leader));
+  if (L < 0) return;
+  const int nc = uniform(*reinterpret_cast<volatile int*>(&ctl.nc));
+  int seq = 0;
+  float* lpark = park0 + (size_t)L * slab;
+  if (nc == NCA) elastic_help<NCA>(el, L, P, lpark, seq);
+  else elastic_help<NCB>(el, L, P, lpark, seq);
+}
+
+// One persistent kernel per register class, kEW waves per workgroup (one per SIMD), elastic
+// teams for the batch tail (see Elastic above).  Each wave drains the larger bin first, then the
+// smaller one, exactly as solve_group_kernel.
+template <int NCA, int NCB>
+__global__ void __launch_bounds__(64 * kEW, Cfg<NCA>::WPE)
+    solve_elastic_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
+                         const int* __restrict__ list_b, const int* __restrict__ counts,
+                         int* __restrict__ heads, int qa, float* __restrict__ work,
+                         size_t slab) {
+  static_assert(Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
+  constexpr size_t kR0 = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
+                                                                : sizeof(Smem<NCB>);
+  constexpr int kR = (int)((kR0 + 15) & ~size_t(15));
+  static_assert(sizeof(TeamSmem<NCA, kEW>) <= (size_t)kR && sizeof(TeamSmem<NCB, kEW>) <= (size_t)kR,
+                "a team block fits an idle wave's instance image");
+  __shared__ __attribute__((aligned(16))) unsigned char raw[kEW * kR];
+  __shared__ ElasticCtl ctl;
+  const int wv = uniform((int)(threadIdx.x >> 6));
+  if (threadIdx.x == 0) {
+    ctl.idle = 0;
+    ctl.leader = -1;
+    ctl.nc = 0;
+  }
+  __syncthreads();
+  float* park0 = work + (size_t)blockIdx.x * kEW * slab;
+  float* park = park0 + (size_t)wv * slab;
+  int seq = 0;
+  bool team = false;
+  const Elastic el{&ctl, raw, kR, wv, &seq, &team};
+  unsigned char* mine = raw + wv * kR;
+#ifdef CMPC_STAMPS
+  Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(mine);
+  if ((threadIdx.x & 63) < 32) s0.st[threadIdx.x & 63] = 0;
+#endif
+  drain_bin<NCA, 1>(*reinterpret_cast<Smem<NCA>*>(mine), P, in, out, list_a, counts + qa,
+                    heads + qa, park, nullptr, nullptr, &el);
+  drain_bin<NCB, 1>(*reinterpret_cast<Smem<NCB>*>(mine), P, in, out, list_b, counts + qa - 1,
+                    heads + qa - 1, park, nullptr, nullptr, &el);
+#ifdef CMPC_STAMPS
+  WSYNC();
+  if ((threadIdx.x & 63) < 32) atomicAdd(&g_stamps[threadIdx.x & 63], s0.st[threadIdx.x & 63]);
+#endif
+  elastic_finish<NCA, NCB>(el, P, park0, slab);
 }
 
 // Team mode (cmpc_team.hip): one workgroup of W waves per QP, one kernel for all four bins

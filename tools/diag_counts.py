@@ -21,13 +21,14 @@ def _lpt(cyc, W):
 def main():
     import torch
     from cmpc import _lib
-    _lib._lib = _lib.load(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_diag.so")
+    import os
+    _lib._lib = _lib.load(os.environ.get("CMPC_DIAG_LIB", str(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_diag.so")))
     from cmpc import Plan, SolverParams, to_device_batch, synth
     over = dict(a.split("=") for a in sys.argv[1:])
     over = {k: type(getattr(SolverParams, k))(float(v) if "." in v else int(v)) for k, v in over.items()}
     plan = Plan(SolverParams(max_batch=65536, **over))
-    for cfg in (1, 2):
-        b = synth.make_batch(65536, seed=cfg, mixed=cfg == 2)
+    for cfg in (1, 2, 3):
+        b = synth.make_config(3) if cfg == 3 else synth.make_batch(65536, seed=cfg, mixed=cfg == 2)
         d = to_device_batch(b)
         w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
         torch.cuda.synchronize()
@@ -48,6 +49,17 @@ def main():
         print(f"  max: cycles {cyc.max():.0f} iters {iters[order[0]]} polish {pol[order[0]]} fact {fac[order[0]]}")
         for q in (50, 90, 99, 99.9):
             print(f"  p{q}: cycles {np.percentile(cyc, q):.0f} iters {np.percentile(iters, q):.0f} fact {np.percentile(fac, q):.0f}")
+        if cfg == 3:  # strong scaling: the slowest instance of each rank's contiguous shard
+            for R in (1, 2, 4, 8):
+                sh = np.array_split(cyc, R)
+                print(f"  {R} ranks: shard max instance {max(x.max() for x in sh):.0f} cycles, "
+                      f"mean per shard {np.mean([x.sum() for x in sh]):.3g}")
+            nc = np.array([int(v) for v in d["contact"].reshape(65536, -1).ne(0).sum(1).cpu()]) * 3
+            for lo, hi in ((0, 96), (97, 128), (129, 160), (161, 192)):
+                m = (nc >= lo) & (nc <= hi)
+                if m.any():
+                    print(f"  bin <= {hi}: {m.sum()} inst, mean cycles {cyc[m].mean():.0f}, "
+                          f"p99 {np.percentile(cyc[m], 99):.0f}, max {cyc[m].max():.0f}")
         if cfg == 1:  # one bin: persistent waves pulling the queue in (about) index order
             import heapq
             W = 2048  # 8 waves per CU x 256 CUs (NC = 128)
