@@ -201,41 +201,70 @@ def timed_steps(step, steps, warmup, sync, barrier, reduce_max):
 # ------------------------------------------------------------------------------------------
 # GPU measurement helpers
 # ------------------------------------------------------------------------------------------
-def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None, counters=None):
+def _counters_of(counters, name):
+    """PMC record of kernel `name` in profiles/*_counters.json (keys are rocprof's demangled
+    names, e.g. 'void cmpc::solve_group_kernel<128, 96>')."""
+    for k, v in (counters or {}).items():
+        if isinstance(v, dict) and k.replace(" ", "").endswith(name.replace(" ", "")):
+            return v
+    return None
+
+
+def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None, counters=None,
+                    step_ms=None):
     """Roofline of the dominant solve kernel of the last timed steps: algorithmic bytes of the
-    solves it processed / its average HIP-event duration (kernels run on their own streams)."""
+    solves it processed / its average HIP-event duration (kernels run on their own streams).
+    The dominant kernel is the one that processes the most solves (config 3: the NC <= 128
+    class, 82 % of the instances; the other class runs concurrently on its own stream).  With
+    PMC counters in profiles/, the compute roofline is the counted MFMA work over the live
+    duration; `step` prices both kernels together over the whole step."""
     kern = kernel_of_bins(bins)
     names = list(KERNEL_NAMES)
     team = hasattr(plan.lib, "cmpc_plan_team_batch") and B_shard <= plan.team_batch()
     if team:  # small batch: one team kernel (four waves per QP) serves every bin
         kern = np.zeros_like(kern)
         names[0] = TEAM_KERNEL_NAME
+    nk = 2 - int(team)
     avg = [ms[k] / max(calls[k], 1) for k in range(2)]
-    q = int(np.argmax(avg))
-    n_q = int(np.sum(kern == q))
+    n_k = [int(np.sum(kern == k)) for k in range(2)]
+    q = int(np.argmax(n_k[:nk]))
+    n_q = n_k[q]
     achieved = BYTES_PER_SOLVE * n_q / (avg[q] * 1e-3) / 1e9 if avg[q] > 0 else 0.0
     flops = algorithmic_flops(contact, iters)
     fl_q = float(flops[kern == q].sum())
     tfs = fl_q / (avg[q] * 1e-3) / 1e12 if avg[q] > 0 else 0.0
+    cq = None if team else _counters_of(counters, names[q])
+    if cq and cq.get("hbm_bytes_per_launch"):
+        traffic = cq["hbm_bytes_per_launch"]  # this kernel's PMC bytes (FETCH x 2 + WRITE)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic if not team else None,
             "kernel": names[q], "kernel_avg_ms": avg[q], "solves_per_launch": n_q,
             "bytes_per_solve": BYTES_PER_SOLVE,
-            "kernel_avg_ms_all": {names[k]: avg[k] for k in range(2 - int(team))},
-            "solves_per_kernel": {names[k]: int(np.sum(kern == k)) for k in range(2 - int(team))}}
+            "kernel_avg_ms_all": {names[k]: avg[k] for k in range(nk)},
+            "solves_per_kernel": {names[k]: n_k[k] for k in range(nk)}}
     comp = {"bound": "mfma", "achieved": tfs, "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tfs / F32_MATRIX_PEAK_TFS, "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
+            "frac": tfs / F32_MATRIX_PEAK_TFS, "kernel": names[q],
+            "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
             "flops_per_solve": fl_q / max(n_q, 1)}
-    c = None if team else ((counters or {}).get(KERNEL_NAMES[q].replace(", ", ","), None) or
-                           (counters or {}).get(KERNEL_NAMES[q], None))
-    if c and c.get("SQ_INSTS_MFMA") and avg[q] > 0:
+    if cq and cq.get("SQ_INSTS_MFMA") and avg[q] > 0:
         # counted matrix work of this kernel per launch (PMC, profiles/) over its live duration
-        ach = c["SQ_INSTS_MFMA"] * 2048.0 / (avg[q] * 1e-3) / 1e12
+        ach = cq["SQ_INSTS_MFMA"] * 2048.0 / (avg[q] * 1e-3) / 1e12
         comp.update(model_achieved=tfs, model_frac=tfs / F32_MATRIX_PEAK_TFS, achieved=ach,
                     frac=ach / F32_MATRIX_PEAK_TFS,
                     basis="SQ_INSTS_MFMA x 2048 FLOP (v_mfma_f32_16x16x4_f32) per launch from "
                           "profiles/r02_counters.json / live kernel time",
-                    mfma_per_launch=c["SQ_INSTS_MFMA"], mfma_busy_frac_pmc=c.get("mfma_busy_frac"))
+                    mfma_per_launch=cq["SQ_INSTS_MFMA"], mfma_busy_frac_pmc=cq.get("mfma_busy_frac"))
+    if step_ms and not team:
+        # both class kernels together over the step (they overlap on two streams)
+        mf = [(_counters_of(counters, names[k]) or {}).get("SQ_INSTS_MFMA") for k in range(nk)]
+        st = {"step_ms": step_ms, "solves": int(sum(n_k[:nk])),
+              "hbm_achieved_GBs": BYTES_PER_SOLVE * sum(n_k[:nk]) / (step_ms * 1e-3) / 1e9}
+        st["hbm_frac"] = st["hbm_achieved_GBs"] / HBM_PEAK_GBS
+        if all(m for m, k in zip(mf, range(nk)) if n_k[k] > 0) and any(mf):
+            tf = sum(m for m in mf if m) * 2048.0 / (step_ms * 1e-3) / 1e12
+            st.update(mfma_achieved_TFs=tf, mfma_frac=tf / F32_MATRIX_PEAK_TFS,
+                      mfma_basis="SQ_INSTS_MFMA of both kernels (profiles/r02_counters.json)")
+        comp["step"] = st
     return roof, comp
 
 
@@ -338,9 +367,11 @@ def main(argv=None):
     bins = bins_of(shard["contact"])
     traffic_j = load_json(args.traffic_json)
     traffic = traffic_j.get("hbm_bytes_per_launch") if traffic_j else None
-    counters = load_json(args.counters_json)
+    # the PMC counters were collected on one full config-3 launch (65,536 solves on one GPU):
+    # per-launch counts apply only to that workload
+    counters = load_json(args.counters_json) if (args.config == 3 and Bs == 65536) else None
     roof, roof_c = kernel_roofline(plan, Bs, bins, shard["contact"], iters, ms_k, calls_k,
-                                   traffic, counters)
+                                   traffic, counters, step_ms=1e3 * elapsed / args.steps)
 
     # ---- N > 1: scatter from rank 0 -> solve -> gather to rank 0 (RCCL over xGMI) ----
     scat = None
