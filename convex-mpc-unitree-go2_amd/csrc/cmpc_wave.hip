@@ -187,7 +187,7 @@ struct Cfg {
   static constexpr int THREADS = 64;             // one wave per QP
   // per wave (floats): park slab of the inverse, then the ADMM state (x, z, y) kept aside
   // during the interior-point fallback (ipm_save)
-  static constexpr int SLAB = NTL * 256 + 3 * NC;
+  static constexpr int SLAB = NTL * 256 + 3 * NC + 20 * 64;
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
   static constexpr int WPE = CMPC_WPE_OVERRIDE;
 };
@@ -1296,22 +1296,33 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 // Interior-point identification of the face set, for hard instances.  A few instances per
 // thousand keep ADMM's face set "stable" but wrong for a long time: their polish sessions fail,
 // repair, fail again, and the instance runs 100-200 ADMM iterations and 20-45 factorizations
-// (5-10 M cycles), which sets the time of any batch or shard that holds one.  After kIpmAfter
-// failed sessions such an instance runs kIpmIters Mehrotra predictor-corrector steps on the
-// condensed QP
+// (5-10 M cycles), which sets the time of any batch or shard that holds one.  Once an instance
+// has failed kIpmAfter sessions and spent kIpmFacts factorizations, it runs kIpmIters Mehrotra
+// predictor-corrector steps on the condensed QP
 //     min 1/2 u'Pu + q'u   s.t.  G_t u_t <= h_t per stance triple (the 5 pyramid rows),
-// keeping the slacks s = h - G u exact (u stays strictly inside K) and solving each Newton
-// system (P + G' diag(z/s) G) du = rhs with the fp32 inverse of that matrix (P parked once, the
-// 3x3 barrier block of every triple added to the tiles, the 4-pivot sweep).  Its face set (rows
-// with multiplier z > slack s) then starts a polish session with the full repair budget.
-// Prototyped in NumPy on the slowest config-3 instances: after 11 fp32 steps the polish +
-// repairs need 1-5 factorizations (ADMM had needed 20-45).
+// from the interior point (0, 0, 2 fz_min), keeping the slacks as their own variables (s + G u
+// = h to rounding) and solving each Newton system (P + G' diag(z/s) G) du = rhs with the fp32
+// inverse of that matrix (P parked once, the 3x3 barrier block of every triple added to the
+// tiles, the 4-pivot sweep).  Its face set (rows with multiplier z > slack s) then starts a
+// polish session with the full repair budget; if that fails too, ADMM resumes exactly where it
+// was.  Prototyped in NumPy on the slowest config-3 instances (after 11 fp32 steps the polish +
+// repairs need 1-5 factorizations where ADMM had needed 20-45).  The steps cost ~14
+// factorizations, so the trigger is late: measured config 2 at B = 4,096 +35 %,
+// the slowest config-3 instances 8-12 M -> 4 M cycles, ~2 % on easy large batches (code size).
 // ------------------------------------------------------------------------------------------
 #ifndef CMPC_IPM_AFTER
-#define CMPC_IPM_AFTER 0  // failed polish sessions before the interior-point fallback (0: never)
+#define CMPC_IPM_AFTER 1  // failed polish sessions before the interior-point fallback (0: never)
+#endif
+#ifndef CMPC_IPM_FACTS
+#define CMPC_IPM_FACTS 16  // ... and factorizations spent so far (the fallback costs ~14)
 #endif
 constexpr int kIpmAfter = CMPC_IPM_AFTER;
+constexpr int kIpmFacts = CMPC_IPM_FACTS;
 constexpr int kIpmIters = 11;
+#ifndef CMPC_IPM_MU_STOP
+#define CMPC_IPM_MU_STOP 0.f  // stop once mu < this x the first mu (0: run kIpmIters steps)
+#endif
+constexpr float kIpmMuStop = CMPC_IPM_MU_STOP;
 
 __device__ __forceinline__ float wave_sum(float v) { return col4_sum(row16_sum(v)); }
 __device__ __forceinline__ float wave_min(float v) { return -wave_max(-v); }
@@ -1381,8 +1392,29 @@ __device__ __forceinline__ float ipm_maxstep(const float (&v)[5], const float (&
   return a;
 }
 
+// Per-lane interior-point state (the 5 multipliers z and slacks s of the lane's triple, and the
+// predictor's ds, dz) lives in global memory at the tail of the wave's park slab, lane-major:
+// nothing of it is held in registers across the condensation, the sweep or a symv, which need
+// the whole register file (holding it there spilled ~80 VGPRs into the one-wave kernel and cost
+// the hot path ~9 % on config 1).
+constexpr int kIpmKeep = 20 * 64;  // floats: z, s, ds_aff, dz_aff x 5 rows x 64 lanes
+
+__device__ __forceinline__ void ipm_ld(const float* __restrict__ st, int slot, int l, float (&v)[5]) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) v[i] = st[(5 * slot + i) * 64 + l];
+}
+__device__ __forceinline__ void ipm_st(float* __restrict__ st, int slot, int l, const float (&v)[5]) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) st[(5 * slot + i) * 64 + l] = v[i];
+}
+// own earlier stores become visible to this wave's loads
+__device__ __forceinline__ void ipm_sync() {
+  asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
+}
+
 // Leaves the face set in s.code (lane t = triple t), u in s.x and s.z, the multiplier
 // y = G' z in s.y; clobbers the park slab (the ADMM inverse is no longer parked) and M.
+// Returns false if a step went non-finite.
 template <int NC>
 __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
                                              f4 (&M)[Cfg<NC>::NTL], float* __restrict__ park,
@@ -1392,14 +1424,10 @@ __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
   const float mu = P.mu, fzm = P.fz_min;
   n = uniform(n);
   ntri = uniform(ntri);
+  float* st = park + Cfg<NC>::NTL * 256 + 3 * NC;  // slots 0 z, 1 s, 2 ds_aff, 3 dz_aff
   condense_tiles<NC>(s, P, M, n, uniformf(P.sigma));  // P (+ sigma), parked for every step
   park_store<NC>(park, M);
   float* dd = s.y;  // z / s of row i of triple t at dd[i * ntri + t] (5 ntri <= 2 NC floats)
-  // multipliers and slacks of this lane's triple.  The slacks are their own variables, moved
-  // by the same steps as u (s + G u = h holds to rounding): recomputing h - G u would cancel
-  // a small slack of an active row to nothing in fp32 (measured on the NumPy transcription:
-  // non-finite steps and wrong face sets).
-  float zc[5], sl[5];
   {
     const int l = opaque_lane();
     WSYNC();
@@ -1408,37 +1436,55 @@ __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
       s.x[3 * l + 1] = 0.f;
       s.x[3 * l + 2] = 2.f * fzm;
     }
-    float gu[5];
+    // The slacks are their own variables, moved by the same steps as u (s + G u = h holds to
+    // rounding): recomputing h - G u would cancel a small slack of an active row to nothing in
+    // fp32 (NumPy transcription: non-finite steps and wrong face sets).
+    float gu[5], zc[5], sl[5];
     ipm_rows(0.f, 0.f, 2.f * fzm, mu, fzm, gu);
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
       zc[i] = (l < ntri) ? 1.f : 0.f;
       sl[i] = (l < ntri) ? -gu[i] : 1.f;
     }
+    ipm_st(st, 0, l, zc);
+    ipm_st(st, 1, l, sl);
   }
   const float m_inv = 1.f / (5.f * (float)max(ntri, 1));
+  float mu_first = 0.f;
   for (int it = 0; it < kIpmIters; ++it) {
     gradient<NC>(s, P, n, s.x, s.g);  // grad f(u)
-    const int l = opaque_lane();
-    const bool own = l < ntri;
-    WSYNC();
-    float sz = 0.f;
+    float mu_c;
+    {
+      const int l = opaque_lane();
+      ipm_sync();
+      float zc[5], sl[5];
+      ipm_ld(st, 0, l, zc);
+      ipm_ld(st, 1, l, sl);
+      WSYNC();
+      float sz = 0.f;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      sz += sl[i] * zc[i];
-      if (own) dd[i * ntri + l] = zc[i] / sl[i];
+      for (int i = 0; i < 5; ++i) {
+        sz += sl[i] * zc[i];
+        if (l < ntri) dd[i * ntri + l] = zc[i] / sl[i];
+      }
+      mu_c = uniformf(wave_sum(sz) * m_inv);
     }
-    const float mu_c = wave_sum(sz) * m_inv;
+    if (it == 0) mu_first = mu_c;
+    if (it > 0 && mu_c < kIpmMuStop * mu_first) break;  // (uniform) identified well enough
     park_load<NC>(park, M);
     ipm_add_barrier<NC>(s, M, n, ntri, mu, dd);
     invert_tiles<NC>(s, M, n);
     // predictor: rhs = -grad f (the slacks are exact, so the primal residual is zero)
-    for (int p = l; p < n; p += 64) s.r[p] = -s.g[p];
+    for (int p = opaque_lane(); p < n; p += 64) s.r[p] = -s.g[p];
     symv<NC>(s, M, n, s.r, s.dl);
-    float dsa[5], dza[5];
+    float smu;
     {
+      const int l = opaque_lane();
+      const bool own = l < ntri;
+      float zc[5], sl[5], dsa[5], dza[5], gd[5];
+      ipm_ld(st, 0, l, zc);
+      ipm_ld(st, 1, l, sl);
       WSYNC();
-      float gd[5];
       ipm_gdir(own ? s.dl[3 * l] : 0.f, own ? s.dl[3 * l + 1] : 0.f, own ? s.dl[3 * l + 2] : 0.f,
                mu, gd);
 #pragma unroll
@@ -1446,31 +1492,42 @@ __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
         dsa[i] = own ? -gd[i] : 0.f;
         dza[i] = own ? -zc[i] - zc[i] * dsa[i] / sl[i] : 0.f;
       }
-    }
-    const float apa = wave_min(ipm_maxstep(sl, dsa)), ada = wave_min(ipm_maxstep(zc, dza));
-    float sza = 0.f;
+      const float apa = wave_min(ipm_maxstep(sl, dsa)), ada = wave_min(ipm_maxstep(zc, dza));
+      float sza = 0.f;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) sza += (sl[i] + apa * dsa[i]) * (zc[i] + ada * dza[i]);
-    const float mu_a = wave_sum(own ? sza : 0.f) * m_inv;
-    const float rat = mu_a / fmaxf(mu_c, 1e-30f);
-    const float smu = rat * rat * rat * mu_c;  // sigma mu (Mehrotra's centring)
-    // corrector: rhs = -grad f + G' ((dsa dza - sigma mu) / s)
-    float wv[5];
+      for (int i = 0; i < 5; ++i) sza += (sl[i] + apa * dsa[i]) * (zc[i] + ada * dza[i]);
+      const float mu_a = wave_sum(own ? sza : 0.f) * m_inv;
+      const float rat = mu_a / fmaxf(mu_c, 1e-30f);
+      smu = uniformf(rat * rat * rat * mu_c);  // sigma mu (Mehrotra's centring)
+      // corrector: rhs = -grad f + G' ((dsa dza - sigma mu) / s)
+      float wv[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) wv[i] = (dsa[i] * dza[i] - smu) / sl[i];
-    WSYNC();
-    if (own) {
-      s.r[3 * l] = -s.g[3 * l] + (wv[1] - wv[2]);
-      s.r[3 * l + 1] = -s.g[3 * l + 1] + (wv[3] - wv[4]);
-      s.r[3 * l + 2] = -s.g[3 * l + 2] - wv[0] - mu * (wv[1] + wv[2] + wv[3] + wv[4]);
+      for (int i = 0; i < 5; ++i) wv[i] = (dsa[i] * dza[i] - smu) / sl[i];
+      if (own) {
+        s.r[3 * l] = -s.g[3 * l] + (wv[1] - wv[2]);
+        s.r[3 * l + 1] = -s.g[3 * l + 1] + (wv[3] - wv[4]);
+        s.r[3 * l + 2] = -s.g[3 * l + 2] - wv[0] - mu * (wv[1] + wv[2] + wv[3] + wv[4]);
+      }
+      ipm_st(st, 2, l, dsa);
+      ipm_st(st, 3, l, dza);
+#ifdef CMPC_TRACE
+      if (tr && l == 0) printf("  ipm %d mu %g mu_aff %g steps aff %g %g\n", it, mu_c, mu_a, apa, ada);
+#endif
     }
     symv<NC>(s, M, n, s.r, s.dl);
-    float du[3], ds[5], dz[5];
+    bool stop;
     {
+      const int l = opaque_lane();
+      const bool own = l < ntri;
+      ipm_sync();
+      float zc[5], sl[5], dsa[5], dza[5], du[3], ds[5], dz[5], gd[5];
+      ipm_ld(st, 0, l, zc);
+      ipm_ld(st, 1, l, sl);
+      ipm_ld(st, 2, l, dsa);
+      ipm_ld(st, 3, l, dza);
       WSYNC();
 #pragma unroll
       for (int a = 0; a < 3; ++a) du[a] = own ? s.dl[3 * l + a] : 0.f;
-      float gd[5];
       ipm_gdir(du[0], du[1], du[2], mu, gd);
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
@@ -1478,27 +1535,34 @@ __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
         const float rc = sl[i] * zc[i] + dsa[i] * dza[i] - smu;
         dz[i] = own ? (-zc[i] * ds[i] - rc) / sl[i] : 0.f;
       }
-    }
-    const float ap = 0.99f * wave_min(ipm_maxstep(sl, ds)), ad = 0.99f * wave_min(ipm_maxstep(zc, dz));
+      const float ap = 0.99f * wave_min(ipm_maxstep(sl, ds)), ad = 0.99f * wave_min(ipm_maxstep(zc, dz));
 #ifdef CMPC_TRACE
-    if (tr && l == 0)
-      printf("  ipm %d mu %g mu_aff %g steps aff %g %g steps %g %g\n", it, mu_c, mu_a, apa, ada, ap, ad);
+      if (tr && l == 0) printf("  ipm %d steps %g %g\n", it, ap, ad);
 #endif
-    // a collapsed step is fp32 running out near the end: keep the last iterate
-    if (it > 0 && ap < 0.1f) break;
-    WSYNC();
-    if (own) {
+      // a collapsed step is fp32 running out near the end: keep the last iterate
+      stop = it > 0 && ap < 0.1f;
+      if (!stop) {
+        if (own) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) s.x[3 * l + a] += ap * du[a];
-    }
+          for (int a = 0; a < 3; ++a) s.x[3 * l + a] += ap * du[a];
+        }
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      zc[i] += ad * dz[i];
-      sl[i] += ap * ds[i];
+        for (int i = 0; i < 5; ++i) {
+          zc[i] += ad * dz[i];
+          sl[i] += ap * ds[i];
+        }
+        ipm_st(st, 0, l, zc);
+        ipm_st(st, 1, l, sl);
+      }
     }
+    if (stop) break;  // (uniform)
   }
   // the face set (rows whose multiplier exceeds their slack), the point and its multiplier
   const int l = opaque_lane();
+  ipm_sync();
+  float zc[5], sl[5];
+  ipm_ld(st, 0, l, zc);
+  ipm_ld(st, 1, l, sl);
   WSYNC();
   bool bad = false;
   if (l < ntri) {
@@ -1520,10 +1584,6 @@ __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
     s.y[3 * l + 2] = -zc[0] - mu * (zc[1] + zc[2] + zc[3] + zc[4]);
     bad = !(isfinite(ux) && isfinite(uy) && isfinite(uz) && isfinite(s.y[3 * l]) &&
             isfinite(s.y[3 * l + 1]) && isfinite(s.y[3 * l + 2]));
-#ifdef CMPC_TRACE
-    if (tr) printf("  ipm lane %d code %d z %g %g %g %g %g s %g %g %g %g %g\n", l, s.code[l], zc[0], zc[1],
-                   zc[2], zc[3], zc[4], sl[0], sl[1], sl[2], sl[3], sl[4]);
-#endif
   }
   WSYNC();
   return __any(bad) == 0;
@@ -1809,6 +1869,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int last_pol = 0;       // iteration of the last polish session
   bool ipm_done = false;  // the interior-point fallback ran (at most once per instance)
   int nsfail = 0;         // failed sessions, remembered starts included
+  int nfact = 0;          // factorizations so far
   int nseen = 0;          // sessions in a row that started from a remembered set
   bool ipm_session = false;  // the current polish session started from its face set
   const float alpha = P.alpha;
@@ -1827,6 +1888,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   while (n > 0) {
     if (refactor) {  // the only condense + invert call site
       CMPC_CNT(8, 1);
+      ++nfact;
 #ifdef CMPC_DIAG_COUNTS
       ++dg_fact;
 #endif
@@ -1949,10 +2011,13 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
       }
       if constexpr (W == 1 && kIpmAfter > 0) {
-        if (!eteam && !ipm_done && nsfail >= kIpmAfter) {
+        if (!eteam && !ipm_done && nsfail >= kIpmAfter && nfact >= kIpmFacts) {
           // a hard instance: identify the face set by interior-point steps, then polish it
           // with the full repair budget (ADMM resumes where it was if that session fails too)
           ipm_done = true;
+#ifdef CMPC_DIAG_COUNTS
+          dg_pol += 100;  // (diagnostic: the interior-point fallback ran)
+#endif
           float* keep = park + Cfg<NC>::NTL * 256;
           ipm_save<NC>(s, keep, n);
 #ifdef CMPC_TRACE

@@ -1,6 +1,7 @@
 """Diagnostic: per-instance cost anatomy (libcmpc_diag.so, -DCMPC_DIAG_COUNTS): iterations,
 polish attempts, factorizations and wave cycles per instance; how much of the batch's wave time
 the slowest instances take."""
+import os
 import sys
 from pathlib import Path
 
@@ -21,7 +22,6 @@ def _lpt(cyc, W):
 def main():
     import torch
     from cmpc import _lib
-    import os
     _lib._lib = _lib.load(os.environ.get("CMPC_DIAG_LIB", str(REPO / "convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_diag.so")))
     from cmpc import Plan, SolverParams, to_device_batch, synth
     over = dict(a.split("=") for a in sys.argv[1:])
@@ -35,6 +35,8 @@ def main():
         cyc = st.cpu().numpy().astype(np.float64) * 16
         code = it.cpu().numpy().astype(np.int64)
         iters, pol, fac = code % 1000, (code // 1000) % 1000, code // 1000000
+        if os.environ.get("CMPC_DIAG_SAVE"):
+            np.savez_compressed(f"{os.environ['CMPC_DIAG_SAVE']}_cfg{cfg}.npz", cyc=cyc, code=code)
         order = np.argsort(-cyc)
         tot = cyc.sum()
         print(f"cfg{cfg} {over}: mean cycles {cyc.mean():.0f}  iters mean {iters.mean():.2f}  "
