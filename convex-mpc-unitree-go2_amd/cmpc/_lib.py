@@ -11,7 +11,7 @@ from pathlib import Path
 
 from .build import LIB
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 CMPC_OK = 0
 
 
@@ -34,6 +34,7 @@ class CParams(ctypes.Structure):
         ("polish_refine", ctypes.c_int32),
         ("polish_tol", ctypes.c_float),
         ("polish_repairs", ctypes.c_int32),
+        ("ipm_facts", ctypes.c_int32),
         ("max_batch", ctypes.c_int64),
     ]
 

@@ -134,6 +134,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_refine = 4;
   p->polish_tol = 1e-5f;
   p->polish_repairs = 6;
+  p->ipm_facts = 16;
   p->max_batch = 65536;
 }
 
@@ -155,7 +156,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (!(p->rho > 0.f) || !(p->sigma >= 0.f) || !(p->alpha > 0.f && p->alpha < 2.f))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: need rho > 0, sigma >= 0, 0 < alpha < 2");
   if (p->polish_stable < 1 || p->polish_refine < 1 || !(p->polish_tol > 0.f) ||
-      p->polish_repairs < 0)
+      p->polish_repairs < 0 || p->ipm_facts < 0)
     return fail(CMPC_E_INVALID, "cmpc_plan_create: polish settings out of range");
   if (p->adaptive_rho_interval < 0 || p->max_batch < 1 || p->max_batch > (1LL << 30))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: adaptive_rho_interval/max_batch out of range");
@@ -181,6 +182,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   k.polish_stable = p->polish_stable;
   k.polish_refine = p->polish_refine;
   k.polish_repairs = p->polish_repairs;
+  k.ipm_facts = p->ipm_facts;
 
   hipError_t e = hipGetDevice(&pl->device);
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipGetDevice"); }

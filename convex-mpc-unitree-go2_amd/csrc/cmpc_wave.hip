@@ -1297,7 +1297,7 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 // thousand keep ADMM's face set "stable" but wrong for a long time: their polish sessions fail,
 // repair, fail again, and the instance runs 100-200 ADMM iterations and 20-45 factorizations
 // (5-10 M cycles), which sets the time of any batch or shard that holds one.  Once an instance
-// has failed kIpmAfter sessions and spent kIpmFacts factorizations, it runs kIpmIters Mehrotra
+// has failed kIpmAfter sessions and spent P.ipm_facts factorizations, it runs kIpmIters Mehrotra
 // predictor-corrector steps on the condensed QP
 //     min 1/2 u'Pu + q'u   s.t.  G_t u_t <= h_t per stance triple (the 5 pyramid rows),
 // from the interior point (0, 0, 2 fz_min), keeping the slacks as their own variables (s + G u
@@ -1313,11 +1313,7 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 #ifndef CMPC_IPM_AFTER
 #define CMPC_IPM_AFTER 1  // failed polish sessions before the interior-point fallback (0: never)
 #endif
-#ifndef CMPC_IPM_FACTS
-#define CMPC_IPM_FACTS 16  // ... and factorizations spent so far (the fallback costs ~14)
-#endif
-constexpr int kIpmAfter = CMPC_IPM_AFTER;
-constexpr int kIpmFacts = CMPC_IPM_FACTS;
+constexpr int kIpmAfter = CMPC_IPM_AFTER;  // (and KParams.ipm_facts factorizations spent)
 constexpr int kIpmIters = 11;
 #ifndef CMPC_IPM_MU_STOP
 #define CMPC_IPM_MU_STOP 0.f  // stop once mu < this x the first mu (0: run kIpmIters steps)
@@ -2011,7 +2007,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
       }
       if constexpr (W == 1 && kIpmAfter > 0) {
-        if (!eteam && !ipm_done && nsfail >= kIpmAfter && nfact >= kIpmFacts) {
+        if (!eteam && !ipm_done && P.ipm_facts > 0 && nsfail >= kIpmAfter && nfact >= P.ipm_facts) {
           // a hard instance: identify the face set by interior-point steps, then polish it
           // with the full repair budget (ADMM resumes where it was if that session fails too)
           ipm_done = true;

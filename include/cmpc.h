@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 1
+#define CMPC_ABI_VERSION 2
 
 #define CMPC_OK 0
 #define CMPC_E_INVALID (-22)   /* bad argument / parameter (EINVAL) */
@@ -77,6 +77,9 @@ typedef struct cmpc_params {
   float polish_tol;       /* relative KKT tolerance for accepting the polished point */
   int32_t polish_repairs; /* active-set repairs (add violated / drop negative-multiplier faces
                              and re-polish) before resuming ADMM */
+  int32_t ipm_facts;      /* an instance that has failed a polish session and spent this many
+                             factorizations identifies its face set by interior-point steps
+                             (hard instances); 0 = never.  Default 16 */
   int64_t max_batch;      /* largest B passed to cmpc_solve (sizes plan workspace) */
 } cmpc_params;
 
