@@ -42,6 +42,7 @@ class CParams(ctypes.Structure):
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
            "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_plan_set_team", "cmpc_plan_team_batch",
+           "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch",
            "cmpc_last_error",
            "cmpc_version")
 NUM_BINS = 4
@@ -102,6 +103,11 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
         lib.cmpc_plan_set_team.restype = ctypes.c_int
         lib.cmpc_plan_team_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         lib.cmpc_plan_team_batch.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_plan_set_ipm"):
+        lib.cmpc_plan_set_ipm.argtypes = [vp, ctypes.c_int64]
+        lib.cmpc_plan_set_ipm.restype = ctypes.c_int
+        lib.cmpc_plan_ipm_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+        lib.cmpc_plan_ipm_batch.restype = ctypes.c_int
     lib.cmpc_last_error.argtypes = []
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_version.argtypes = []

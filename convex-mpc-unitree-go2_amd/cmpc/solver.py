@@ -133,6 +133,19 @@ class Plan:
                "cmpc_plan_team_batch")
         return int(v.value)
 
+    def set_ipm(self, max_batch: int):
+        """Kernel variants with the interior-point fallback for solves of B <= max_batch (above
+        the team bound): -1 = automatic (B <= 64 x CUs, the default), 0 = never
+        (cmpc_plan_set_ipm)."""
+        _check(self.lib, self.lib.cmpc_plan_set_ipm(self._h, int(max_batch)), "cmpc_plan_set_ipm")
+
+    def ipm_batch(self) -> int:
+        """The largest batch solved by the fallback-carrying kernels (cmpc_plan_ipm_batch)."""
+        v = ctypes.c_int64()
+        _check(self.lib, self.lib.cmpc_plan_ipm_batch(self._h, ctypes.byref(v)),
+               "cmpc_plan_ipm_batch")
+        return int(v.value)
+
     def timing_read(self):
         """-> (ms_per_kernel[2], calls_per_kernel[2]) of the two solve kernels since the last
         read (kernel 0: bins NC 128 + 96; kernel 1: bins NC 192 + 160, _lib.KERNEL_BINS)."""

@@ -37,6 +37,9 @@ struct cmpc_plan {
   int team_grid = 0;
   size_t team_slab = 0;
   int64_t team_max_batch = -1;  // -1: automatic (B <= 4 x CUs: at most one wave per SIMD)
+  // tail-bound batches (B <= ipm_max_batch): the one-wave kernel variants with the
+  // interior-point fallback for hard instances
+  int64_t ipm_max_batch = -1;   // -1: automatic (B <= 64 x CUs)
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -90,10 +93,12 @@ constexpr int kTeamWaves = 4;
 #endif
 constexpr int kGroupWaves = CMPC_ELASTIC ? cmpc::kEW : 1;
 
-KernelFn group_fn(int k) {
+KernelFn group_fn(int k, bool ipm = false) {
   if (CMPC_ELASTIC)
     return k == 0 ? cmpc::solve_elastic_kernel<128, 96> : cmpc::solve_elastic_kernel<192, 160>;
-  return k == 0 ? cmpc::solve_group_kernel<128, 96> : cmpc::solve_group_kernel<192, 160>;
+  if (ipm)
+    return k == 0 ? cmpc::solve_group_kernel<128, 96, true> : cmpc::solve_group_kernel<192, 160, true>;
+  return k == 0 ? cmpc::solve_group_kernel<128, 96, false> : cmpc::solve_group_kernel<192, 160, false>;
 }
 
 // park slab per wave (floats): the one-wave inverse, or (elastic) a whole team's slots
@@ -296,8 +301,13 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
                     cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
 }
 
+static int64_t ipm_batch(const cmpc_plan* pl) {
+  return pl->ipm_max_batch >= 0 ? pl->ipm_max_batch : 64LL * pl->cus;
+}
+
 static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParams& kp,
-                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
+                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g,
+                         bool ipm) {
   hipError_t e;
   cmpc_plan::Rec rec{nullptr, nullptr, k};
   const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
@@ -313,7 +323,7 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64 * kGroupWaves), 0, s, kp, in, out,
+  hipLaunchKernelGGL(group_fn(k, ipm), dim3(g), dim3(64 * kGroupWaves), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
@@ -393,18 +403,20 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
+  // tail-bound batch: the kernel variants with the interior-point fallback
+  const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
 #ifndef CMPC_CLASS_ORDER
 #define CMPC_CLASS_ORDER 0
 #endif
   if (CMPC_CLASS_ORDER == 1 && big) {  // heavy class on the caller's stream, light one forked after
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, st, kp, in, out, g1);
+    rc = record_launch(pl, 1, st, kp, in, out, g1, ipm);
     if (rc != CMPC_OK) return rc;
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
     const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-    rc = record_launch(pl, 0, pl->side, kp, in, out, g0);
+    rc = record_launch(pl, 0, pl->side, kp, in, out, g0, ipm);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
@@ -412,22 +424,22 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   }
   if (CMPC_CLASS_ORDER == 2 && big) {  // serialised: heavy class, then light class
     const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, st, kp, in, out, g1);
+    rc = record_launch(pl, 1, st, kp, in, out, g1, ipm);
     if (rc != CMPC_OK) return rc;
     const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-    return record_launch(pl, 0, st, kp, in, out, g0);
+    return record_launch(pl, 0, st, kp, in, out, g0, ipm);
   }
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
     const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, pl->side, kp, in, out, g1);
+    rc = record_launch(pl, 1, pl->side, kp, in, out, g1, ipm);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-  rc = record_launch(pl, 0, st, kp, in, out, g0);
+  rc = record_launch(pl, 0, st, kp, in, out, g0, ipm);
   if (rc != CMPC_OK) return rc;
   if (big && (e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
     return hip_fail(e, "hipStreamWaitEvent");
@@ -546,6 +558,19 @@ int cmpc_plan_set_team(cmpc_plan* pl, int64_t max_batch) {
 int cmpc_plan_team_batch(const cmpc_plan* pl, int64_t* max_batch) {
   if (!pl || !max_batch) return fail(CMPC_E_INVALID, "cmpc_plan_team_batch: null argument");
   *max_batch = team_batch(pl);
+  return CMPC_OK;
+}
+
+int cmpc_plan_set_ipm(cmpc_plan* pl, int64_t max_batch) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_ipm: null plan");
+  if (max_batch < -1) return fail(CMPC_E_INVALID, "cmpc_plan_set_ipm: max_batch must be >= -1");
+  pl->ipm_max_batch = max_batch;
+  return CMPC_OK;
+}
+
+int cmpc_plan_ipm_batch(const cmpc_plan* pl, int64_t* max_batch) {
+  if (!pl || !max_batch) return fail(CMPC_E_INVALID, "cmpc_plan_ipm_batch: null argument");
+  *max_batch = ipm_batch(pl);
   return CMPC_OK;
 }
 

@@ -1409,8 +1409,11 @@ __device__ __forceinline__ void ipm_sync() {
 }
 
 // Leaves the face set in s.code (lane t = triple t), u in s.x and s.z, the multiplier
-// y = G' z in s.y; clobbers the park slab (the ADMM inverse is no longer parked) and M.
-// Returns false if a step went non-finite.
+// y = G' z in s.y; clobbers the park slab (the ADMM inverse is no longer parked) and M.  Returns
+// false if a step went non-finite.  (Inlined into the one-wave kernels it costs registers on the
+// hot path -- ~70 VGPR spills, 3.4 GB more HBM writes per config-3 launch -- so only the kernel
+// variants for tail-bound batches carry it, solve_group_kernel<.., .., true>; as a called
+// function the caller's tiles went to scratch: 1.8x slower.)
 template <int NC>
 __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
                                              f4 (&M)[Cfg<NC>::NTL], float* __restrict__ park,
@@ -1701,7 +1704,8 @@ __device__ __forceinline__ bool tried_before(Smem<NC>& s, int ntri, int ntried) 
 }
 
 // ------------------------------------------------------------------------------------------
-template <int NC, int W>
+// IPM: this kernel variant carries the interior-point fallback (tail-bound batches)
+template <int NC, int W, bool IPM = false>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
                                                float* __restrict__ park, TeamSmem<NC, W>* ts,
@@ -2006,7 +2010,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         ipm_session = false;
         ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
       }
-      if constexpr (W == 1 && kIpmAfter > 0) {
+      if constexpr (W == 1 && IPM && kIpmAfter > 0) {
         if (!eteam && !ipm_done && P.ipm_facts > 0 && nsfail >= kIpmAfter && nfact >= P.ipm_facts) {
           // a hard instance: identify the face set by interior-point steps, then polish it
           // with the full repair budget (ADMM resumes where it was if that session fails too)
@@ -2302,7 +2306,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 
 // Drain one bin's queue with this wave (persistent: instance ids come from a device counter).
 // (W > 1: the leader's loop; the helpers leave their command loop at the closing kOpExit)
-template <int NC, int W>
+template <int NC, int W, bool IPM = false>
 __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const Inputs& in,
                                           const Outputs& out, const int* __restrict__ list,
                                           const int* __restrict__ count, int* __restrict__ head,
@@ -2320,7 +2324,7 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
     if (lane == 0) idx = atomicAdd(head, 1);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= total) break;
-    solve_instance<NC, W>(s, P, (int64_t)list[idx], in, out, park, ts, seq, el);
+    solve_instance<NC, W, IPM>(s, P, (int64_t)list[idx], in, out, park, ts, seq, el);
   }
   if constexpr (W > 1) team_issue<NC, W>(*ts, *seq, kOpExit, 0, 0, 0);
 }
@@ -2329,8 +2333,9 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
 // SIMD for NC <= 128, one for NC >= 160), so one kernel serves both, draining the larger bin
 // first (its instances are the slower ones: hardest first shortens the batch tail).  Two
 // kernels instead of four keep the solve within the device's hardware queues (the caller's
-// stream + one plan stream), so the two classes really overlap.
-template <int NCA, int NCB>
+// stream + one plan stream), so the two classes really overlap.  IPM: the variant with the
+// interior-point fallback for hard instances (used for tail-bound batches).
+template <int NCA, int NCB, bool IPM>
 __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
     solve_group_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
                        const int* __restrict__ list_b, const int* __restrict__ counts,
@@ -2346,10 +2351,10 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
   Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(raw);
   if (threadIdx.x < 32) s0.st[threadIdx.x] = 0;
 #endif
-  drain_bin<NCA, 1>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa,
-                    heads + qa, park);
-  drain_bin<NCB, 1>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
-                    heads + qa - 1, park);
+  drain_bin<NCA, 1, IPM>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa,
+                         heads + qa, park);
+  drain_bin<NCB, 1, IPM>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
+                         heads + qa - 1, park);
 #ifdef CMPC_STAMPS
   WSYNC();
   if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);

@@ -247,6 +247,15 @@ int cmpc_plan_set_timing(cmpc_plan* plan, int enable);
  * it for B <= 4 x CUs; 0 disables it.  cmpc_plan_team_batch returns the effective bound. */
 int cmpc_plan_set_team(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
+
+/* Tail-bound batches.  A batch of B <= max_batch instances (one wave per QP, i.e. above the
+ * small-batch bound) runs the kernel variants that carry the interior-point fallback for hard
+ * instances (cmpc_params.ipm_facts): a small batch or an N-GPU shard takes as long
+ * as its slowest instance, which the fallback shortens 2-3x.  Large batches run the variants
+ * without it (its code costs registers on the hot path).  max_batch = -1 (the default) selects
+ * B <= 64 x CUs; 0 never.  cmpc_plan_ipm_batch returns the effective bound. */
+int cmpc_plan_set_ipm(cmpc_plan* plan, int64_t max_batch);
+int cmpc_plan_ipm_batch(const cmpc_plan* plan, int64_t* max_batch);
 int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_kernel, int32_t* calls_per_kernel);
 
 /* Thread-local description of the last error returned on this thread ("" if none). */

@@ -1,8 +1,8 @@
 """GPU parity of the interior-point face-set identification (cmpc_wave.hip ipm_identify,
 DESIGN.md 4h) against the KKT-certified optimum.
 
-The default plan runs it only on the few hard instances of a batch (a failed polish session and
-16 factorizations).  These tests force it early (ipm_facts = 1: after the first failed session)
+The default plan runs it only on the few hard instances of tail-bound batches (B <= 64 x CUs,
+cmpc_plan_set_ipm; a failed polish session and 16 factorizations).  These tests force it early (ipm_facts = 1: after the first failed session)
 so that every instance whose first polish session fails -- ~1-2 % of config 2 / 3 -- goes
 through the interior-point steps, the polish session they start and, when that fails, the
 restored ADMM state.  Tolerance as in test_gpu_parity.py: max |U - U*| / max |U*| <= 1e-4.
@@ -19,7 +19,9 @@ TOL_U = 1e-4
 @pytest.fixture(scope="module")
 def plan_ipm():
     from cmpc import Plan, SolverParams
-    return Plan(SolverParams(max_batch=65536, ipm_facts=1))
+    p = Plan(SolverParams(max_batch=65536, ipm_facts=1))
+    p.set_ipm(65536)  # the fallback-carrying kernels at every size (default: B <= 64 x CUs)
+    return p
 
 
 def test_hard_cases_forced(plan_ipm):
@@ -66,6 +68,7 @@ def test_full_batch_forced(plan_ipm):
     err = rel_err_U(w[idx], fx["w"])
     assert err.max() <= TOL_U, (err.max(), int(idx[int(err.argmax())]))
     off = Plan(SolverParams(max_batch=65536, ipm_facts=0))
+    off.set_ipm(65536)
     _, st0, it0 = solve_batch(b, plan=off)
     assert np.all(st0 == 1)
     assert it.max() < it0.max(), (int(it.max()), int(it0.max()))
