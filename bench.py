@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import socket
 import subprocess
@@ -133,6 +134,8 @@ def parse(argv=None):
                     help="SolverParams override key=value (experiments)")
     ap.add_argument("--team", type=int, default=-1,
                     help="small-batch team mode for B <= this (cmpc_plan_set_team): -1 auto, 0 off")
+    ap.add_argument("--ipm", type=int, default=-1,
+                    help="interior-point fallback kernels for B <= this (cmpc_plan_set_ipm): -1 auto")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     a = ap.parse_args(argv)
@@ -204,8 +207,10 @@ def timed_steps(step, steps, warmup, sync, barrier, reduce_max):
 def _counters_of(counters, name):
     """PMC record of kernel `name` in profiles/*_counters.json (keys are rocprof's demangled
     names, e.g. 'void cmpc::solve_group_kernel<128, 96>')."""
+    def norm(n):  # the IPM template flag (<.., .., false>) is not part of the bench's label
+        return re.sub(r",(true|false)>", ">", n.replace(" ", ""))
     for k, v in (counters or {}).items():
-        if isinstance(v, dict) and k.replace(" ", "").endswith(name.replace(" ", "")):
+        if isinstance(v, dict) and norm(k).endswith(norm(name)):
             return v
     return None
 
@@ -340,6 +345,8 @@ def main(argv=None):
     plan = Plan(SolverParams(max_batch=max_b, **over), device=dev)
     if args.team != -1 and hasattr(plan.lib, "cmpc_plan_set_team"):
         plan.set_team(args.team)
+    if args.ipm != -1 and hasattr(plan.lib, "cmpc_plan_set_ipm"):
+        plan.set_ipm(args.ipm)
     stream = torch.cuda.current_stream(dev)
     d = to_device_batch(shard, dev)
     w = torch.empty((Bs, 24 * 16), dtype=torch.float32, device=dev)

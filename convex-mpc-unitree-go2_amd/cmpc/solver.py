@@ -39,7 +39,7 @@ class SolverParams:
     polish_refine: int = 4
     polish_tol: float = 1e-5
     polish_repairs: int = 6
-    ipm_facts: int = 16
+    ipm_facts: int = 8
     max_batch: int = 65536
 
     def to_c(self) -> _lib.CParams:

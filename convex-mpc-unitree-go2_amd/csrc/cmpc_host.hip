@@ -139,7 +139,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_refine = 4;
   p->polish_tol = 1e-5f;
   p->polish_repairs = 6;
-  p->ipm_facts = 16;
+  p->ipm_facts = 8;
   p->max_batch = 65536;
 }
 

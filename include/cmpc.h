@@ -79,7 +79,7 @@ typedef struct cmpc_params {
                              and re-polish) before resuming ADMM */
   int32_t ipm_facts;      /* an instance that has failed a polish session and spent this many
                              factorizations identifies its face set by interior-point steps
-                             (hard instances); 0 = never.  Default 16 */
+                             (hard instances); 0 = never.  Default 8 */
   int64_t max_batch;      /* largest B passed to cmpc_solve (sizes plan workspace) */
 } cmpc_params;
 

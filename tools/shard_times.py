@@ -2,6 +2,7 @@
 global batch (65,536) alone, for N = 1, 2, 4, 8 ranks (cmpc.dist.shard_bounds).  A multi-GPU
 step takes as long as its slowest shard, so max over shards is the N-GPU step time."""
 import functools
+import os
 import sys
 from pathlib import Path
 
@@ -15,12 +16,14 @@ sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 def main():
     import torch
     from cmpc import _lib
-    if len(sys.argv) > 1:
+    if len(sys.argv) > 1 and sys.argv[1]:
         _lib._lib = _lib.load(sys.argv[1])
     from cmpc import Plan, SolverParams, to_device_batch, synth
     from cmpc.dist import shard_bounds
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    plan = Plan(SolverParams(max_batch=65536))
+    # IPM_FACTS: the interior-point trigger (SolverParams.ipm_facts) for trigger sweeps
+    facts = int(os.environ.get("IPM_FACTS", SolverParams.ipm_facts))
+    plan = Plan(SolverParams(max_batch=65536, ipm_facts=facts))
     d = to_device_batch(synth.make_config(3))
     B = d["Ad"].shape[0]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
