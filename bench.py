@@ -54,9 +54,8 @@ HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s
 F32_MATRIX_PEAK_TFS = 157.3                      # MI355X_MICROARCH.md: dense f32 MFMA peak
 POLISH_REFINE = 4                                # SolverParams.polish_refine (default)
 GLOBAL_BATCH = {1: 256, 2: 4096, 3: 65536}       # BASELINE.json configs[1..3]
-KERNEL_BINS = ((1, 0), (3, 2))                   # cmpc/_lib.py: kernel k serves these bins
+# solve kernels of builds without cmpc_plan_solve_kernel (two register-class kernels)
 KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<192, 160>")
-TEAM_KERNEL_NAME = "solve_team_kernel<4>"  # B <= Plan.team_batch(): all bins, 4 waves per QP
 
 
 def algorithmic_flops(contact, iters, N=16):
@@ -217,50 +216,64 @@ def _counters_of(counters, name):
 
 def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None, counters=None,
                     step_ms=None):
-    """Roofline of the dominant solve kernel of the last timed steps: algorithmic bytes of the
-    solves it processed / its average HIP-event duration (kernels run on their own streams).
-    The dominant kernel is the one that processes the most solves (config 3: the NC <= 128
-    class, 82 % of the instances; the other class runs concurrently on its own stream).  With
-    PMC counters in profiles/, the compute roofline is the counted MFMA work over the live
-    duration; `step` prices both kernels together over the whole step."""
-    kern = kernel_of_bins(bins)
-    names = list(KERNEL_NAMES)
-    team = hasattr(plan.lib, "cmpc_plan_team_batch") and B_shard <= plan.team_batch()
-    if team:  # small batch: one team kernel (four waves per QP) serves every bin
-        kern = np.zeros_like(kern)
-        names[0] = TEAM_KERNEL_NAME
-    nk = 2 - int(team)
+    """Rooflines of the solve kernels of the last timed steps: algorithmic bytes of the solves a
+    kernel processed / its average HIP-event duration (measured on the stream it runs on).
+    Returns (roofline, roofline_compute, roofline_critical):
+      * roofline / roofline_compute: the DOMINANT kernel, the one that processes the most solves;
+      * roofline_critical: the kernel whose live time sets the step (the longest average launch),
+        with its HBM and compute fractions and its share of the step.  With one solve kernel per
+        launch (the pair kernel, or the team kernel for small batches) both are the same kernel.
+    With PMC counters in profiles/, the compute roofline is the counted MFMA work over the live
+    duration; `step` prices every launched kernel together over the whole step."""
+    names = plan.solve_kernels(B_shard)
+    if names[0] is None:  # an older A/B build without cmpc_plan_solve_kernel: two class kernels
+        names = list(KERNEL_NAMES)
+    kern = kernel_of_bins(bins) if names[1] is not None else np.zeros_like(bins)
+    nk = 2 if names[1] is not None else 1
     avg = [ms[k] / max(calls[k], 1) for k in range(2)]
     n_k = [int(np.sum(kern == k)) for k in range(2)]
-    q = int(np.argmax(n_k[:nk]))
-    n_q = n_k[q]
-    achieved = BYTES_PER_SOLVE * n_q / (avg[q] * 1e-3) / 1e9 if avg[q] > 0 else 0.0
+    q = int(np.argmax(n_k[:nk]))                 # dominant: most solves
+    c = int(np.argmax(avg[:nk]))                 # critical: longest live time
     flops = algorithmic_flops(contact, iters)
-    fl_q = float(flops[kern == q].sum())
-    tfs = fl_q / (avg[q] * 1e-3) / 1e12 if avg[q] > 0 else 0.0
-    cq = None if team else _counters_of(counters, names[q])
-    if cq and cq.get("hbm_bytes_per_launch"):
-        traffic = cq["hbm_bytes_per_launch"]  # this kernel's PMC bytes (FETCH x 2 + WRITE)
-    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic if not team else None,
-            "kernel": names[q], "kernel_avg_ms": avg[q], "solves_per_launch": n_q,
-            "bytes_per_solve": BYTES_PER_SOLVE,
-            "kernel_avg_ms_all": {names[k]: avg[k] for k in range(nk)},
-            "solves_per_kernel": {names[k]: n_k[k] for k in range(nk)}}
-    comp = {"bound": "mfma", "achieved": tfs, "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": tfs / F32_MATRIX_PEAK_TFS, "kernel": names[q],
-            "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
-            "flops_per_solve": fl_q / max(n_q, 1)}
-    if cq and cq.get("SQ_INSTS_MFMA") and avg[q] > 0:
-        # counted matrix work of this kernel per launch (PMC, profiles/) over its live duration
-        ach = cq["SQ_INSTS_MFMA"] * 2048.0 / (avg[q] * 1e-3) / 1e12
-        comp.update(model_achieved=tfs, model_frac=tfs / F32_MATRIX_PEAK_TFS, achieved=ach,
-                    frac=ach / F32_MATRIX_PEAK_TFS,
-                    basis="SQ_INSTS_MFMA x 2048 FLOP (v_mfma_f32_16x16x4_f32) per launch from "
-                          "profiles/r02_counters.json / live kernel time",
-                    mfma_per_launch=cq["SQ_INSTS_MFMA"], mfma_busy_frac_pmc=cq.get("mfma_busy_frac"))
+    team = names[0].startswith("solve_team")
+
+    def hbm(k):
+        achieved = BYTES_PER_SOLVE * n_k[k] / (avg[k] * 1e-3) / 1e9 if avg[k] > 0 else 0.0
+        ck = None if team else _counters_of(counters, names[k])
+        tr = ck.get("hbm_bytes_per_launch") if ck else (traffic if (k == q and not team) else None)
+        return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": tr, "kernel": names[k],
+                "kernel_avg_ms": avg[k], "solves_per_launch": n_k[k],
+                "bytes_per_solve": BYTES_PER_SOLVE}
+
+    def compute(k):
+        fl = float(flops[kern == k].sum())
+        tfs = fl / (avg[k] * 1e-3) / 1e12 if avg[k] > 0 else 0.0
+        comp = {"bound": "mfma", "achieved": tfs, "peak": F32_MATRIX_PEAK_TFS, "unit": "TFLOP/s",
+                "frac": tfs / F32_MATRIX_PEAK_TFS, "kernel": names[k],
+                "basis": "algorithmic FLOP model (bench.algorithmic_flops)",
+                "flops_per_solve": fl / max(n_k[k], 1)}
+        ck = None if team else _counters_of(counters, names[k])
+        if ck and ck.get("SQ_INSTS_MFMA") and avg[k] > 0:
+            # counted matrix work of this kernel per launch (PMC, profiles/) over its live duration
+            ach = ck["SQ_INSTS_MFMA"] * 2048.0 / (avg[k] * 1e-3) / 1e12
+            comp.update(model_achieved=tfs, model_frac=tfs / F32_MATRIX_PEAK_TFS, achieved=ach,
+                        frac=ach / F32_MATRIX_PEAK_TFS,
+                        basis="SQ_INSTS_MFMA x 2048 FLOP (v_mfma_f32_16x16x4_f32) per launch from "
+                              "the profiles/ counters / live kernel time",
+                        mfma_per_launch=ck["SQ_INSTS_MFMA"], mfma_busy_frac_pmc=ck.get("mfma_busy_frac"))
+        return comp
+
+    roof = hbm(q)
+    roof.update(kernel_avg_ms_all={names[k]: avg[k] for k in range(nk)},
+                solves_per_kernel={names[k]: n_k[k] for k in range(nk)})
+    comp = compute(q)
+    crit = hbm(c)
+    crit["compute"] = compute(c)
+    crit["step_share"] = avg[c] / step_ms if step_ms else None
+    crit["same_as_dominant"] = c == q
     if step_ms and not team:
-        # both class kernels together over the step (they overlap on two streams)
+        # every launched solve kernel together over the step
         mf = [(_counters_of(counters, names[k]) or {}).get("SQ_INSTS_MFMA") for k in range(nk)]
         st = {"step_ms": step_ms, "solves": int(sum(n_k[:nk])),
               "hbm_achieved_GBs": BYTES_PER_SOLVE * sum(n_k[:nk]) / (step_ms * 1e-3) / 1e9}
@@ -268,9 +281,9 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
         if all(m for m, k in zip(mf, range(nk)) if n_k[k] > 0) and any(mf):
             tf = sum(m for m in mf if m) * 2048.0 / (step_ms * 1e-3) / 1e12
             st.update(mfma_achieved_TFs=tf, mfma_frac=tf / F32_MATRIX_PEAK_TFS,
-                      mfma_basis="SQ_INSTS_MFMA of both kernels (profiles/r02_counters.json)")
+                      mfma_basis="SQ_INSTS_MFMA of the launched kernels (profiles/ counters)")
         comp["step"] = st
-    return roof, comp
+    return roof, comp, crit
 
 
 def load_json(path):
@@ -377,8 +390,9 @@ def main(argv=None):
     # the PMC counters were collected on one full config-3 launch (65,536 solves on one GPU):
     # per-launch counts apply only to that workload
     counters = load_json(args.counters_json) if (args.config == 3 and Bs == 65536) else None
-    roof, roof_c = kernel_roofline(plan, Bs, bins, shard["contact"], iters, ms_k, calls_k,
-                                   traffic, counters, step_ms=1e3 * elapsed / args.steps)
+    roof, roof_c, roof_crit = kernel_roofline(plan, Bs, bins, shard["contact"], iters, ms_k,
+                                              calls_k, traffic, counters,
+                                              step_ms=1e3 * elapsed / args.steps)
 
     # ---- N > 1: scatter from rank 0 -> solve -> gather to rank 0 (RCCL over xGMI) ----
     scat = None
@@ -446,7 +460,8 @@ def main(argv=None):
             plan.set_timing(False)
             mk, ck = plan.timing_read()
             itb = ib.cpu().numpy()
-            r, rc = kernel_roofline(plan, B, bins_of(b["contact"]), b["contact"], itb, mk, ck)
+            r, rc, rcrit = kernel_roofline(plan, B, bins_of(b["contact"]), b["contact"], itb, mk,
+                                           ck, step_ms=el / ksteps * 1e3)
             configs[name] = {"solves_per_s": B * ksteps / el, "ms_per_step": el / ksteps * 1e3,
                              "batch": B, "steps": ksteps,
                              "solved_frac": float((sb == 1).float().mean().item()),
@@ -454,16 +469,24 @@ def main(argv=None):
                              "roofline": {k: r[k] for k in ("achieved", "frac", "kernel",
                                                             "kernel_avg_ms", "kernel_avg_ms_all",
                                                             "solves_per_kernel")},
-                             "roofline_compute_frac": rc["frac"]}
+                             "roofline_compute_frac": rc["frac"],
+                             "roofline_critical": {k: rcrit[k] for k in ("kernel", "kernel_avg_ms",
+                                                                         "frac", "step_share")}}
             del db, wb, sb, ib
 
     aux = {}
     if world == 1:
-        aux = aux_objects(args, plan, full, dev, stream, torch)
+        if args.aux:
+            aux["shard_rehearsal"] = shard_rehearsal(plan, d, GB, stream, torch)
+        aux.update(aux_objects(args, plan, full, dev, stream, torch))
 
     cpu = None
+    odist = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(full, args.cpu_seconds)
+        w_osqp = cpu.pop("_w", None)
+        if w_osqp is not None:
+            odist = osqp_distance(full, w.cpu().numpy(), w_osqp, cpu["cores"])
 
     if rank == 0:
         line = {
@@ -491,7 +514,9 @@ def main(argv=None):
             "ranks_reporting": n_ranks,
             "roofline": roof,
             "roofline_compute": roof_c,
+            "roofline_critical": roof_crit,
             "cpu_baseline": cpu,
+            "osqp_distance": odist,
             "solved_frac": solved / GB,
             "iters_mean": float(np.mean(iters)),
             "iters_max": int(np.max(iters)),
@@ -804,6 +829,69 @@ def aux_objects(args, plan, full, dev, stream, torch):
             "solve_time_ms": float(np.median(st_ms)), "update_time_ms": float(np.median(up_ms)),
             "wall_ms_per_tick": float(np.median(wall)), "mpc_dt_budget_ms": 1e3 / 48,
             "return_status": mpc.solver.stats()["return_status"]}
+    return out
+
+
+def _rel_u(wa, wb, N=16):
+    """max_k,leg |U_a - U_b| / max |U_b| per instance (the parity metric of tests/)."""
+    ua, ub = np.asarray(wa, np.float64)[:, 12 * N:], np.asarray(wb, np.float64)[:, 12 * N:]
+    return np.abs(ua - ub).max(1) / np.maximum(np.abs(ub).max(1), 1e-12)
+
+
+def osqp_distance(full, w_gpu, w_osqp, cores, n_tight=256):
+    """Informational: how far this solver's forces are from what the
+    reference's OSQP solve returns, on the cpu_baseline sample, and how far that OSQP output
+    (reference OPTS, eps 1e-4) is from the optimum -- the optimum being the same restatement run
+    to eps 1e-10 on the first n_tight instances.  The parity bar (tests/) is against the
+    KKT-certified optimum."""
+    from oracle import osqp_ref
+    n = w_osqp.shape[0]
+    wg = w_gpu[:n]
+    m = min(n, n_tight)
+    sub = {k: v[:m] for k, v in full.items() if isinstance(v, np.ndarray)}
+    rt = osqp_ref.solve_batch(sub, threads=cores, settings=osqp_ref.tight_settings())
+    ok = rt["status"] == 1
+
+    def stats(e):
+        return {"median": float(np.median(e)), "max": float(np.max(e)),
+                "p90": float(np.percentile(e, 90))} if len(e) else None
+    return {"metric": "max |U_a - U_b| / max |U_b| per instance (forces u_0..u_15)",
+            "gpu_vs_osqp_ref": stats(_rel_u(wg, w_osqp)), "sample": int(n),
+            "osqp_ref_vs_optimum": stats(_rel_u(w_osqp[:m], rt["w"])[ok]),
+            "gpu_vs_optimum": stats(_rel_u(wg[:m], rt["w"])[ok]),
+            "optimum_sample": int(m), "optimum_converged_frac": float(ok.mean()),
+            "optimum": "oracle/osqp_ref.cpp at eps 1e-10 (converges to the KKT-certified optimum)",
+            "osqp_ref": "oracle/osqp_ref.cpp with the reference OPTS (centroidal_mpc.py:20-36)"}
+
+
+def shard_rehearsal(plan, d, GB, stream, torch, reps=5):
+    """Strong-scaling rehearsal on one GPU: every rank's contiguous shard of
+    the global batch (cmpc.dist.shard_bounds) solved alone, median of `reps` HIP-event-timed
+    solves each.  An N-GPU step lasts as long as its slowest shard, so the predicted speedup at
+    N is (N = 1 time) / max over the N shards."""
+    from cmpc.dist import shard_bounds
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = {"method": "each shard of the config's global batch solved alone on this GPU, median "
+                     f"of {reps}; step(N) = max over the N shards", "N": {}}
+    base = None
+    for R in (1, 2, 4, 8):
+        ms = []
+        for r in range(R):
+            lo, hi = shard_bounds(GB, r, R)
+            args = [d[k][lo:hi] for k in ("Ad", "Bd", "gd", "x0", "xref", "contact")]
+            plan.solve(*args, stream=stream)
+            t = []
+            for _ in range(reps):
+                e0.record(stream)
+                plan.solve(*args, stream=stream)
+                e1.record(stream)
+                e1.synchronize()
+                t.append(e0.elapsed_time(e1))
+            ms.append(float(np.median(t)))
+        step = max(ms)
+        base = step if base is None else base
+        out["N"][str(R)] = {"shard_ms": ms, "step_ms": step, "predicted_speedup": base / step,
+                            "predicted_solves_per_s": GB / (step * 1e-3)}
     return out
 
 

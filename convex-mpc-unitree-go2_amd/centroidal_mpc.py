@@ -29,8 +29,8 @@ NX = 12
 NU = 12
 FZ_MIN = 10.0  # centroidal_mpc.py:127
 
-# centroidal_mpc.py:20-36 (the reference's OSQP options; eps/max_iter/adaptive interval map
-# onto cmpc_params, the rest are OSQP-internal and have no counterpart)
+# centroidal_mpc.py:20-36 (the reference's OSQP options; eps/max_iter/adaptive interval and
+# check_termination map onto cmpc_params, the rest are OSQP-internal and have no counterpart)
 OPTS = {
     'warm_start_primal': True,
     'warm_start_dual': True,
@@ -82,7 +82,8 @@ class CentroidalMPC:
             N=traj.N, Q=tuple(np.diag(self.Q)), R=tuple(np.diag(self.R)), mu=MU, fz_min=FZ_MIN,
             eps_abs=OPTS["osqp"]["eps_abs"], eps_rel=OPTS["osqp"]["eps_rel"],
             max_iter=OPTS["osqp"]["max_iter"],
-            adaptive_rho_interval=OPTS["osqp"]["adaptive_rho_interval"], max_batch=1)
+            adaptive_rho_interval=OPTS["osqp"]["adaptive_rho_interval"],
+            check_termination=OPTS["osqp"]["check_termination"], max_batch=1)
         self.plan = Plan(p, device=device)
         self.solver = _SolverHandle()
         import torch

@@ -11,7 +11,7 @@ from pathlib import Path
 
 from .build import LIB
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 CMPC_OK = 0
 
 
@@ -35,6 +35,7 @@ class CParams(ctypes.Structure):
         ("polish_tol", ctypes.c_float),
         ("polish_repairs", ctypes.c_int32),
         ("ipm_facts", ctypes.c_int32),
+        ("check_termination", ctypes.c_int32),
         ("max_batch", ctypes.c_int64),
     ]
 
@@ -42,7 +43,7 @@ class CParams(ctypes.Structure):
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
            "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_plan_set_team", "cmpc_plan_team_batch",
-           "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch",
+           "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch", "cmpc_plan_solve_kernel",
            "cmpc_last_error",
            "cmpc_version")
 NUM_BINS = 4
@@ -108,6 +109,9 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
         lib.cmpc_plan_set_ipm.restype = ctypes.c_int
         lib.cmpc_plan_ipm_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         lib.cmpc_plan_ipm_batch.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_plan_solve_kernel"):
+        lib.cmpc_plan_solve_kernel.argtypes = [vp, ctypes.c_int64, ctypes.c_int]
+        lib.cmpc_plan_solve_kernel.restype = ctypes.c_char_p
     lib.cmpc_last_error.argtypes = []
     lib.cmpc_last_error.restype = ctypes.c_char_p
     lib.cmpc_version.argtypes = []

@@ -40,6 +40,7 @@ class SolverParams:
     polish_tol: float = 1e-5
     polish_repairs: int = 6
     ipm_facts: int = 8
+    check_termination: int = 1   # OPTS check_termination (reference: 10; include/cmpc.h)
     max_batch: int = 65536
 
     def to_c(self) -> _lib.CParams:
@@ -145,6 +146,17 @@ class Plan:
         _check(self.lib, self.lib.cmpc_plan_ipm_batch(self._h, ctypes.byref(v)),
                "cmpc_plan_ipm_batch")
         return int(v.value)
+
+    def solve_kernels(self, B: int) -> list:
+        """Names of the solve kernels a batch of B launches, per timing slot (None: slot not
+        launched), as cmpc_plan_solve_kernel reports them."""
+        if not hasattr(self.lib, "cmpc_plan_solve_kernel"):  # (older A/B builds)
+            return [None] * _lib.NUM_SOLVE_KERNELS
+        out = []
+        for k in range(_lib.NUM_SOLVE_KERNELS):
+            r = self.lib.cmpc_plan_solve_kernel(self._h, int(B), k)
+            out.append(r.decode() if r else None)
+        return out
 
     def timing_read(self):
         """-> (ms_per_kernel[2], calls_per_kernel[2]) of the two solve kernels since the last

@@ -40,6 +40,12 @@ struct cmpc_plan {
   // tail-bound batches (B <= ipm_max_batch): the one-wave kernel variants with the
   // interior-point fallback for hard instances
   int64_t ipm_max_batch = -1;   // -1: automatic (B <= 64 x CUs)
+  // large batches: one two-wave-workgroup kernel for every bin (cmpc_wave.hip solve_pair_kernel)
+  // or the two register-class kernels on two streams (solve_group_kernel)
+  bool pair = true;
+  int pair_grid = 0;
+  size_t pair_slab = 0;       // per workgroup (floats)
+  size_t pair_wave_slab = 0;  // a light wave's share of it
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -86,32 +92,21 @@ int group_first_bin(int k) { return k == 0 ? 1 : 3; }
 
 constexpr int kTeamWaves = 4;
 
-// Elastic workgroups (cmpc_wave.hip solve_elastic_kernel: kEW waves, each its own instances,
-// the batch tail in team mode) or one wave per workgroup (solve_group_kernel).
-#ifndef CMPC_ELASTIC
-#define CMPC_ELASTIC 0
-#endif
-constexpr int kGroupWaves = CMPC_ELASTIC ? cmpc::kEW : 1;
-
 KernelFn group_fn(int k, bool ipm = false) {
-  if (CMPC_ELASTIC)
-    return k == 0 ? cmpc::solve_elastic_kernel<128, 96> : cmpc::solve_elastic_kernel<192, 160>;
   if (ipm)
     return k == 0 ? cmpc::solve_group_kernel<128, 96, true> : cmpc::solve_group_kernel<192, 160, true>;
   return k == 0 ? cmpc::solve_group_kernel<128, 96, false> : cmpc::solve_group_kernel<192, 160, false>;
 }
 
-// park slab per wave (floats): the one-wave inverse, or (elastic) a whole team's slots
-template <int NC>
-constexpr size_t wave_slab() {
-  return CMPC_ELASTIC ? std::max(cmpc::Cfg<NC>::SLAB, cmpc::TeamCfg<NC, cmpc::kEW>::SLAB)
-                      : cmpc::Cfg<NC>::SLAB;
+// park slab per wave (floats): the one-wave inverse (+ the interior-point state)
+size_t group_slab(int k) {
+  return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
+                : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
 }
 
-size_t group_slab(int k) {
-  return k == 0 ? std::max(wave_slab<128>(), wave_slab<96>())
-                : std::max(wave_slab<192>(), wave_slab<160>());
-}
+using PairFn = void (*)(cmpc::KParams, cmpc::Inputs, cmpc::Outputs, const int*, int64_t,
+                        const int*, int*, float*, size_t, size_t);
+PairFn pair_fn(bool ipm) { return ipm ? cmpc::solve_pair_kernel<true> : cmpc::solve_pair_kernel<false>; }
 }  // namespace
 
 extern "C" {
@@ -140,6 +135,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_tol = 1e-5f;
   p->polish_repairs = 6;
   p->ipm_facts = 8;
+  p->check_termination = 1;  // (reference OPTS: 10, accepted; see include/cmpc.h)
   p->max_batch = 65536;
 }
 
@@ -161,7 +157,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (!(p->rho > 0.f) || !(p->sigma >= 0.f) || !(p->alpha > 0.f && p->alpha < 2.f))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: need rho > 0, sigma >= 0, 0 < alpha < 2");
   if (p->polish_stable < 1 || p->polish_refine < 1 || !(p->polish_tol > 0.f) ||
-      p->polish_repairs < 0 || p->ipm_facts < 0)
+      p->polish_repairs < 0 || p->ipm_facts < 0 || p->check_termination < 1)
     return fail(CMPC_E_INVALID, "cmpc_plan_create: polish settings out of range");
   if (p->adaptive_rho_interval < 0 || p->max_batch < 1 || p->max_batch > (1LL << 30))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: adaptive_rho_interval/max_batch out of range");
@@ -188,6 +184,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   k.polish_refine = p->polish_refine;
   k.polish_repairs = p->polish_repairs;
   k.ipm_facts = p->ipm_facts;
+  k.check_every = p->check_termination;
 
   hipError_t e = hipGetDevice(&pl->device);
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipGetDevice"); }
@@ -195,12 +192,18 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pl->device);
   pl->cus = cus;
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
+  // persistent grids: resident workgroups per CU x CUs, the smaller of the kernel variants
+  // without and with the interior-point fallback (both are launched with the same grid)
   size_t work_floats = 0;
   for (int k = 0; k < kNumGroups; ++k) {
-    int nb = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64 * kGroupWaves, 0);
-    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
-    if (nb < 1) nb = 1;
+    int nb = 1 << 30;
+    for (int v = 0; v < 2; ++v) {
+      int b = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, group_fn(k, v == 1), 64, 0);
+      if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+      nb = std::min(nb, b);
+    }
+    if (nb < 1) { delete pl; return fail(CMPC_E_HIP, "cmpc_plan_create: solve kernel cannot be resident"); }
 #ifdef CMPC_STAMPS
     if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
       const int c = atoi(cap);
@@ -210,7 +213,23 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     pl->grid[k] = nb * cus;
     pl->slab[k] = group_slab(k);
     pl->work_off[k] = work_floats;
-    work_floats += (size_t)pl->grid[k] * kGroupWaves * pl->slab[k];
+    work_floats += (size_t)pl->grid[k] * pl->slab[k];
+  }
+  {
+    int nb = 1 << 30;
+    for (int v = 0; v < 2; ++v) {
+      int b = 0;
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, pair_fn(v == 1), 128, 0);
+      if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+      nb = std::min(nb, b);
+    }
+    if (nb < 1) { delete pl; return fail(CMPC_E_HIP, "cmpc_plan_create: pair kernel cannot be resident"); }
+    pl->pair_grid = nb * cus;
+    pl->pair_wave_slab = std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB);
+    pl->pair_slab = std::max({2 * pl->pair_wave_slab, (size_t)cmpc::TeamCfg<192, 2>::SLAB,
+                              (size_t)cmpc::TeamCfg<160, 2>::SLAB});
+    work_floats = std::max(work_floats, (size_t)pl->pair_grid * pl->pair_slab);
+    if (const char* m = getenv("CMPC_SOLVE_KERNEL")) pl->pair = strcmp(m, "group") != 0;
   }
   {
     int nb = 0;
@@ -238,15 +257,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
-  // (A high-priority queue for the one-wave-per-SIMD class, so its waves are placed first, was
-  // measured: within noise on config 3, -1..-4 % on config 2; off unless CMPC_SIDE_PRIORITY_ON.)
-  int prio_least = 0, prio_greatest = 0;
-  (void)prio_least;
-#ifdef CMPC_SIDE_PRIORITY_ON
-  e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-  if (e != hipSuccess) { prio_least = prio_greatest = 0; (void)hipGetLastError(); }
-#endif
-  if ((e = hipStreamCreateWithPriority(&pl->side, hipStreamNonBlocking, prio_greatest)) != hipSuccess ||
+  if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->join, hipEventDisableTiming)) != hipSuccess) {
     cmpc_plan_destroy(pl);
@@ -323,7 +334,7 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(group_fn(k, ipm), dim3(g), dim3(64 * kGroupWaves), 0, s, kp, in, out,
+  hipLaunchKernelGGL(group_fn(k, ipm), dim3(g), dim3(64), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
@@ -371,6 +382,38 @@ static int record_team_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams&
   return CMPC_OK;
 }
 
+// large batches: every bin in one launch of the two-wave-workgroup kernel (timed as kernel 0)
+static int record_pair_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams& kp,
+                              const cmpc::Inputs& in, const cmpc::Outputs& out, int64_t B,
+                              bool ipm) {
+  hipError_t e;
+  cmpc_plan::Rec rec{nullptr, nullptr, 0};
+  const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
+  if (rec_this) {
+    if (!pl->pool.empty()) {
+      rec = pl->pool.back();
+      pl->pool.pop_back();
+      rec.group = 0;
+    } else {
+      if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+      if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+    }
+    if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
+  const int64_t need = (B + 1) / 2;  // two waves per workgroup
+  const unsigned g = (unsigned)(pl->pair_grid < need ? pl->pair_grid : need);
+  hipLaunchKernelGGL(pair_fn(ipm), dim3(g), dim3(128), 0, s, kp, in, out, pl->d_lists,
+                     (int64_t)pl->p.max_batch, pl->d_counters, pl->d_counters + cmpc::kNumBins,
+                     pl->d_work, pl->pair_slab, pl->pair_wave_slab);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "solve_pair_kernel launch");
+  if (rec_this) {
+    if ((e = hipEventRecord(rec.b, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    pl->recs.push_back(rec);
+  }
+  return CMPC_OK;
+}
+
 static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cmpc::Outputs& out,
                       void* stream) {
   int rc = check_device(pl, "cmpc_solve");
@@ -400,35 +443,12 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // stream (measured faster than one wave per QP up to B = 4 x CUs on configs 1-3, slower from
   // 2,048 up: DESIGN.md 4g)
   if (B <= team_batch(pl)) return record_team_launch(pl, st, kp, in, out, B);
+  // tail-bound batch: the kernel variants with the interior-point fallback
+  const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
+  if (pl->pair) return record_pair_launch(pl, st, kp, in, out, B, ipm);
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
-  // tail-bound batch: the kernel variants with the interior-point fallback
-  const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
-#ifndef CMPC_CLASS_ORDER
-#define CMPC_CLASS_ORDER 0
-#endif
-  if (CMPC_CLASS_ORDER == 1 && big) {  // heavy class on the caller's stream, light one forked after
-    if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, st, kp, in, out, g1, ipm);
-    if (rc != CMPC_OK) return rc;
-    if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
-      return hip_fail(e, "hipStreamWaitEvent");
-    const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-    rc = record_launch(pl, 0, pl->side, kp, in, out, g0, ipm);
-    if (rc != CMPC_OK) return rc;
-    if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess) return hip_fail(e, "hipStreamWaitEvent");
-    return CMPC_OK;
-  }
-  if (CMPC_CLASS_ORDER == 2 && big) {  // serialised: heavy class, then light class
-    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, st, kp, in, out, g1, ipm);
-    if (rc != CMPC_OK) return rc;
-    const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-    return record_launch(pl, 0, st, kp, in, out, g0, ipm);
-  }
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
@@ -572,6 +592,16 @@ int cmpc_plan_ipm_batch(const cmpc_plan* pl, int64_t* max_batch) {
   if (!pl || !max_batch) return fail(CMPC_E_INVALID, "cmpc_plan_ipm_batch: null argument");
   *max_batch = ipm_batch(pl);
   return CMPC_OK;
+}
+
+const char* cmpc_plan_solve_kernel(const cmpc_plan* pl, int64_t B, int k) {
+  if (!pl || B < 1 || k < 0 || k >= kNumGroups) return nullptr;
+  if (B <= team_batch(pl)) return k == 0 ? "solve_team_kernel<4>" : nullptr;
+  const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
+  if (pl->pair) return k == 0 ? (ipm ? "solve_pair_kernel<true>" : "solve_pair_kernel<false>") : nullptr;
+  if (k == 1 && !(cmpc::kBinCap[1] < 12 * pl->kp.N)) return nullptr;
+  if (k == 0) return ipm ? "solve_group_kernel<128, 96, true>" : "solve_group_kernel<128, 96, false>";
+  return ipm ? "solve_group_kernel<192, 160, true>" : "solve_group_kernel<192, 160, false>";
 }
 
 int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_kernel, int32_t* calls_per_kernel) {

@@ -39,14 +39,21 @@ struct TeamCfg {
 
 enum : int { kOpExit = 0, kOpFactor = 1, kOpSymv = 2, kOpParkStore = 3, kOpParkLoad = 4 };
 
+// The phase buffers share one region: the diagonal mirror's scratch is dead once the factor's
+// scaling barrier has passed (the sweep's panel is written after it), and a SYMV command starts
+// at a barrier that every wave reaches only after the previous command's last panel read.
 template <int NC, int W>
 struct TeamSmem {
-  int cmd[2][4];                         // op, n, arg1, arg2 (double-buffered by sequence)
-  alignas(16) float pan[2][NC * 4];      // sweep panel, double-buffered by pivot step
-  alignas(16) float ds[NC];              // unit-diagonal scaling of the sweep
-  alignas(16) float partR[NC / 32][NC];  // symv: row sums of column pair pr's tiles
-  alignas(16) float partC[NC];           // symv: column sums (J < I tiles) landing in chunk J
-  alignas(16) float scr[W][512];         // per-wave 2 x 16 x 16 scratch (diagonal mirror)
+  int cmd[2][4];                           // op, n, arg1, arg2 (double-buffered by sequence)
+  alignas(16) float ds[NC];                // unit-diagonal scaling of the sweep
+  union {
+    alignas(16) float pan[2][NC * 4];      // FACTOR sweep: panel, double-buffered by pivot step
+    struct {
+      alignas(16) float partR[NC / 32][NC];  // SYMV: row sums of column pair pr's tiles
+      alignas(16) float partC[NC];           // SYMV: column sums (J < I tiles) landing in chunk J
+    };
+    alignas(16) float scr[W][512];         // FACTOR diagonal mirror: per-wave 2 x 16 x 16 scratch
+  };
 };
 
 // slot geometry: local pair j of wave w, slot l -> tile (I, J); valid iff the pair exists
@@ -625,18 +632,15 @@ __device__ __forceinline__ void team_issue(TeamSmem<NC, W>& ts, int& seq, int op
 }
 
 // helpers: execute the leader's commands until kOpExit (one bin's drain loop)
-// (started: the barrier of the first command has been passed already -- elastic teams)
 template <int NC, int W, int WV>
 __device__ __forceinline__ void team_helper(Smem<NC>& s, TeamSmem<NC, W>& ts, const KParams& P,
-                                            float* __restrict__ park, int& seq,
-                                            bool started = false) {
+                                            float* __restrict__ park, int& seq) {
   constexpr int w = WV;
   f4 M[TeamCfg<NC, W>::SLOTS];
 #pragma unroll
   for (int t = 0; t < TeamCfg<NC, W>::SLOTS; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
   for (;;) {
-    if (!started) team_barrier();
-    started = false;
+    team_barrier();
     const int* cm = ts.cmd[seq & 1];
     const int op = uniform(cm[0]), a0 = uniform(cm[1]), a1 = uniform(cm[2]);
     ++seq;

@@ -212,10 +212,6 @@ constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least thi
 constexpr int kBackoffCap = 3;       // polish back-off doubles per failed session, up to 8x
 constexpr int kLateRepairs = 3;      // repair budget of the sessions after two failed ones
 constexpr int kFailMem = 4;
-#ifndef CMPC_SEEN_MAX
-#define CMPC_SEEN_MAX 1000  // (A/B: 2 resumes repairs after two remembered-set sessions in a row)
-#endif
-constexpr int kSeenMax = CMPC_SEEN_MAX;  // sessions in a row from remembered sets before repairs resume
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
 
@@ -646,11 +642,8 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
 template <int NC>
 __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
                                                f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
-#ifndef CMPC_BC_ALWAYS
-#define CMPC_BC_ALWAYS 0
-#endif
   if constexpr (NC <= 128) {  // the 1-wave-per-SIMD bins would spill the second form
-    if (CMPC_BC_ALWAYS || P.latency_mode) {  // uniform
+    if (P.latency_mode) {  // uniform
       condense_tiles_bc<NC>(s, P, M, n, shift);
       return;
     }
@@ -1614,53 +1607,13 @@ __device__ __forceinline__ void ipm_restore(Smem<NC>& s, const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------
-// Elastic teams (large batches, solve_elastic_kernel).  The persistent kernel's workgroup is
-// kEW waves, one per SIMD of a CU, each draining the bin queues with instances of its own (one
-// wave per QP, the whole lower triangle in its registers).  A wave that finds the queues empty
-// goes idle at the workgroup barrier.  When every other wave of the workgroup is idle, the last
-// running wave turns them into helpers at its next factorization: from then on its instance runs
-// in team mode (cmpc_team.hip: tiles split over kEW waves, the idle waves' instance images hold
-// the team block).  The batch tail -- the few slow instances that set the time of a small shard
-// -- then runs on four SIMDs instead of one.
-// ------------------------------------------------------------------------------------------
-constexpr int kEW = 4;
-
-struct ElasticCtl {
-  int idle;    // waves of the workgroup with no instance left
-  int leader;  // wave index of the team's leader (-1: no team; the waiting waves exit)
-  int nc;      // bin capacity of the leader's instance
-};
-
-struct Elastic {
-  ElasticCtl* ctl;
-  unsigned char* raw;  // the workgroup's instance images, `region` bytes per wave
-  int region;
-  int wv;              // this wave's index in the workgroup
-  int* seq;            // this wave's team command sequence (team_issue)
-  bool* team;          // this wave leads a team
-};
-
-// the team block of leader L lives in the image of wave L + 1 (idle once the team forms)
-template <int NC>
-__device__ __forceinline__ TeamSmem<NC, kEW>* elastic_team_block(const Elastic* el, int L) {
-  return reinterpret_cast<TeamSmem<NC, kEW>*>(el->raw + ((L + 1) & (kEW - 1)) * el->region);
-}
-
-// the first SLOTS tiles of a one-wave register array, as the team layout's slot array
-template <int NC>
-__device__ __forceinline__ f4 (&team_slots(f4 (&M)[Cfg<NC>::NTL]))[TeamCfg<NC, kEW>::SLOTS] {
-  static_assert(TeamCfg<NC, kEW>::SLOTS <= Cfg<NC>::NTL, "team slots fit the one-wave array");
-  return *reinterpret_cast<f4(*)[TeamCfg<NC, kEW>::SLOTS]>(&M[0]);
-}
-
-// ------------------------------------------------------------------------------------------
 // one QP instance on one wave (W = 1) or led by wave 0 of a W-wave team (cmpc_team.hip)
 // A polish session starts from the face set in s.code: record it as the session's first tried
 // set and look it up among the starting sets of failed sessions.  Returns the session's repair
 // budget (none for a remembered set).
 template <int NC>
 __device__ __forceinline__ int session_start(Smem<NC>& s, const KParams& P, int ntri, int nfail,
-                                             int& ntried, bool& seen, int& nseen) {
+                                             int& ntried, bool& seen) {
   const int l = opaque_lane();
   WSYNC();
   uint8_t c = 0;
@@ -1676,14 +1629,7 @@ __device__ __forceinline__ int session_start(Smem<NC>& s, const KParams& P, int 
     const bool diff = (l < ntri) && (s.fpat[k][l] != c);
     seen |= (__any(diff) == 0);
   }
-  // A remembered set is polished once more without repairs -- but not forever: ADMM can settle
-  // on a remembered set (its true face set, where the polish fails only in fp32), and after
-  // kSeenMax such sessions in a row the set gets repairs again (as a new failed session)
-  if (seen) {
-    if (++nseen <= kSeenMax) return 0;
-    seen = false;
-  }
-  nseen = 0;
+  if (seen) return 0;  // a remembered set is polished once more, without repairs
   // after two failed sessions the repair budget shrinks: a wandering repair sequence costs a
   // factorization per step (cfg1 +1 %, cfg2 +1-2 %)
   return (nfail >= 2) ? min(P.polish_repairs, kLateRepairs) : P.polish_repairs;
@@ -1709,14 +1655,9 @@ template <int NC, int W, bool IPM = false>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
                                                float* __restrict__ park, TeamSmem<NC, W>* ts,
-                                               int* seq, const Elastic* el = nullptr) {
+                                               int* seq) {
   // W = 1: the whole lower triangle in this wave's registers; W > 1: this wave's team slots
   f4 M[TeamCfg<NC, W>::SLOTS];
-  // W = 1 in an elastic workgroup: this instance switches to team mode (the idle waves of the
-  // workgroup as helpers) at a factorization once every other wave is idle; from then on the
-  // matrix lives in the team's slots (the first SLOTS entries of M here)
-  bool eteam = false;
-  TeamSmem<NC, kEW>* ets = nullptr;
   static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
   const int lane = opaque_lane();
   const int N = P.N;
@@ -1870,7 +1811,6 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   bool ipm_done = false;  // the interior-point fallback ran (at most once per instance)
   int nsfail = 0;         // failed sessions, remembered starts included
   int nfact = 0;          // factorizations so far
-  int nseen = 0;          // sessions in a row that started from a remembered set
   bool ipm_session = false;  // the current polish session started from its face set
   const float alpha = P.alpha;
   if (n == 0) status = 1;
@@ -1880,7 +1820,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     // repairs fail, ADMM starts from the warm (x, z, y) as above
     WSYNC();
     if (lane < ntri) s.code[lane] = s.pcode[lane];
-    repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start, nseen);
+    repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
     nact = polish_setup<NC>(s, P, Bg, ntri);
     shift = P.sigma;
     in_polish = true;
@@ -1893,33 +1833,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       ++dg_fact;
 #endif
       if constexpr (W == 1) {
-        if (el != nullptr && !eteam) {
-          const int idle = uniform(*reinterpret_cast<volatile int*>(&el->ctl->idle));
-          if (idle == kEW - 1) {  // every other wave is idle: they become this instance's team
-            eteam = true;
-            parked = false;  // a parked inverse has the one-wave layout: refactor instead
-            ets = elastic_team_block<NC>(el, el->wv);
-            WSYNC();
-            if (lane == 0) {
-              el->ctl->leader = el->wv;
-              el->ctl->nc = NC;
-            }
-            *el->seq = 0;
-            *el->team = true;
-          }
-        }
-        if (eteam) {
-          CMPC_T0(t_c);
-          team_factor_lead<NC, kEW>(s, *ets, *el->seq, P, team_slots<NC>(M), nact, uniformf(shift));
-          CMPC_ACC(0, t_c);
-        } else {
-          CMPC_T0(t_c);
-          condense_tiles<NC>(s, P, M, nact, uniformf(shift));
-          CMPC_ACC(0, t_c);
-          CMPC_T0(t_i);
-          invert_tiles<NC>(s, M, nact);
-          CMPC_ACC(1, t_i);
-        }
+        CMPC_T0(t_c);
+        condense_tiles<NC>(s, P, M, nact, uniformf(shift));
+        CMPC_ACC(0, t_c);
+        CMPC_T0(t_i);
+        invert_tiles<NC>(s, M, nact);
+        CMPC_ACC(1, t_i);
       } else {
         CMPC_T0(t_c);
         team_factor_lead<NC, W>(s, *ts, *seq, P, M, nact, uniformf(shift));
@@ -1936,8 +1855,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       for (int q = 0; q < CMPC_REFINE_N + kRefineExtra; ++q) {
         gradient<NC, (W > 1)>(s, P, nact, s.v, s.g, pwc, twc);
         if constexpr (W == 1) {
-          if (eteam) team_symv_lead<NC, kEW>(s, *ets, *el->seq, team_slots<NC>(M), nact, s.g, s.dl);
-          else symv<NC>(s, M, nact, s.g, s.dl);
+          symv<NC>(s, M, nact, s.g, s.dl);
         } else {
           team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
         }
@@ -2011,7 +1929,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
       }
       if constexpr (W == 1 && IPM && kIpmAfter > 0) {
-        if (!eteam && !ipm_done && P.ipm_facts > 0 && nsfail >= kIpmAfter && nfact >= P.ipm_facts) {
+        if (!ipm_done && P.ipm_facts > 0 && nsfail >= kIpmAfter && nfact >= P.ipm_facts) {
           // a hard instance: identify the face set by interior-point steps, then polish it
           // with the full repair budget (ADMM resumes where it was if that session fails too)
           ipm_done = true;
@@ -2033,7 +1951,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
             continue;
           }
           ipm_session = true;
-          session_start<NC>(s, P, ntri, nfail, ntried, seen_start, nseen);
+          session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
           seen_start = false;
           repairs_left = P.polish_repairs;
           nact = polish_setup<NC>(s, P, Bg, ntri);
@@ -2055,12 +1973,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       shift = uniformf(P.sigma + rho);
       if (parked) {
         if constexpr (W == 1) {
-          if (eteam) {
-            team_issue<NC, kEW>(*ets, *el->seq, kOpParkLoad, 0, 0, 0);
-            team_park_load<NC, kEW, 0>(park, team_slots<NC>(M), 0);
-          } else {
-            park_load<NC>(park, M);
-          }
+          park_load<NC>(park, M);
         } else {
           team_issue<NC, W>(*ts, *seq, kOpParkLoad, 0, 0, 0);
           team_park_load<NC, W, 0>(park, M, 0);
@@ -2086,8 +1999,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       }
     }
     if constexpr (W == 1) {
-      if (eteam) team_symv_lead<NC, kEW>(s, *ets, *el->seq, team_slots<NC>(M), n, s.r, s.dl);
-      else symv<NC>(s, M, n, s.r, s.dl);
+      symv<NC>(s, M, n, s.r, s.dl);
     } else {
       team_symv_lead<NC, W>(s, *ts, *seq, M, n, s.r, s.dl);
     }
@@ -2142,7 +2054,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     // back off before a further attempt, longer after failed sessions: both the stable run and
     // the distance to the last session grow as polish_stable x 2^min(nfail, kBackoffCap)
     const int backoff = P.polish_stable << min(nfail, kBackoffCap);
-    if (stable >= P.polish_stable && !last && it - last_pol >= backoff) {
+    if (stable >= P.polish_stable && !last && it - last_pol >= backoff &&
+        (P.check_every == 1 || it % P.check_every == 0)) {  // (OPTS check_termination)
       do_pol = true;
       last_pol = it;
       stable = -backoff;
@@ -2176,12 +2089,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       parked = !refactor && !rho_low && nfail > 0;
       if (parked) {  // restored if the polish fails
         if constexpr (W == 1) {
-          if (eteam) {
-            team_issue<NC, kEW>(*ets, *el->seq, kOpParkStore, 0, 0, 0);
-            team_park_store<NC, kEW, 0>(park, team_slots<NC>(M), 0);
-          } else {
-            park_store<NC>(park, M);
-          }
+          park_store<NC>(park, M);
         } else {
           team_issue<NC, W>(*ts, *seq, kOpParkStore, 0, 0, 0);
           team_park_store<NC, W, 0>(park, M, 0);
@@ -2190,7 +2098,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #else
       parked = false;      // a failed polish refactors the ADMM matrix instead
 #endif
-      repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start, nseen);
+      repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
       nact = polish_setup<NC>(s, P, Bg, ntri);
       CMPC_ACC(14, t_ps);
       shift = P.sigma;
@@ -2293,7 +2201,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     out.iters[b] = iters + 1000 * dg_pol + 1000000 * dg_fact;
 #elif defined(CMPC_DIAG_TIMES)  // start (10 ns ticks, low 31 bits) | duration + 1e9 if teamed
     out.status[b] = (int)(dt_t0 & 0x7fffffffull);
-    out.iters[b] = (int)(__builtin_amdgcn_s_memrealtime() - dt_t0) + (eteam ? 1000000000 : 0);
+    out.iters[b] = (int)(__builtin_amdgcn_s_memrealtime() - dt_t0) ;
 #else
     out.status[b] = status;
     out.iters[b] = iters;
@@ -2311,7 +2219,7 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
                                           const Outputs& out, const int* __restrict__ list,
                                           const int* __restrict__ count, int* __restrict__ head,
                                           float* __restrict__ park, TeamSmem<NC, W>* ts = nullptr,
-                                          int* seq = nullptr, const Elastic* el = nullptr) {
+                                          int* seq = nullptr) {
   const int lane = opaque_lane();
   WSYNC();
   if (lane < 12) {  // KParams copies (each bin's Smem layout places them differently)
@@ -2324,7 +2232,7 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
     if (lane == 0) idx = atomicAdd(head, 1);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= total) break;
-    solve_instance<NC, W, IPM>(s, P, (int64_t)list[idx], in, out, park, ts, seq, el);
+    solve_instance<NC, W, IPM>(s, P, (int64_t)list[idx], in, out, park, ts, seq);
   }
   if constexpr (W > 1) team_issue<NC, W>(*ts, *seq, kOpExit, 0, 0, 0);
 }
@@ -2359,95 +2267,6 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
   WSYNC();
   if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
 #endif
-}
-
-// Elastic workgroup, after this wave's drain loops: a team leader releases its helpers (its
-// instance is done and the queues are empty, so every other wave is idle); any other wave goes
-// idle -- the last one to do so releases the waiting waves, the others wait at the workgroup
-// barrier for the first command of a team (or the release) and then serve as helpers.
-template <int NC>
-__device__ __forceinline__ void elastic_help(const Elastic& el, int L, const KParams& P,
-                                             float* __restrict__ lpark, int& seq) {
-  Smem<NC>& ls = *reinterpret_cast<Smem<NC>*>(el.raw + L * el.region);
-  TeamSmem<NC, kEW>& ts = *elastic_team_block<NC>(&el, L);
-  const int rel = (el.wv - L) & (kEW - 1);  // helper index within the team (the leader is 0)
-  if (rel == 1) team_helper<NC, kEW, 1>(ls, ts, P, lpark, seq, true);
-  else if (rel == 2) team_helper<NC, kEW, 2>(ls, ts, P, lpark, seq, true);
-  else team_helper<NC, kEW, 3>(ls, ts, P, lpark, seq, true);
-}
-
-template <int NCA, int NCB>
-__device__ __forceinline__ void elastic_finish(const Elastic& el, const KParams& P,
-                                               float* __restrict__ park0, size_t slab) {
-  const int lane = opaque_lane();
-  ElasticCtl& ctl = *el.ctl;
-  if (*el.team) {  // (uniform) the leader: release the team
-    if (uniform(ctl.nc) == NCA) team_issue<NCA, kEW>(*elastic_team_block<NCA>(&el, el.wv), *el.seq, kOpExit, 0, 0, 0);
-    else team_issue<NCB, kEW>(*elastic_team_block<NCB>(&el, el.wv), *el.seq, kOpExit, 0, 0, 0);
-    return;
-  }
-  WSYNC();
-  int old = 0;
-  if (lane == 0) old = atomicAdd(&ctl.idle, 1);
-  old = uniform(old);
-  if (old == kEW - 1) {  // the last wave with nothing to lead: release the waiting waves
-    if (lane == 0) ctl.leader = -1;
-    team_barrier();
-    return;
-  }
-  team_barrier();  // the first command of a team, or the release
-  const int L = uniform(*reinterpret_cast<volatile int*>(&ctl.leader));
-  if (L < 0) return;
-  const int nc = uniform(*reinterpret_cast<volatile int*>(&ctl.nc));
-  int seq = 0;
-  float* lpark = park0 + (size_t)L * slab;
-  if (nc == NCA) elastic_help<NCA>(el, L, P, lpark, seq);
-  else elastic_help<NCB>(el, L, P, lpark, seq);
-}
-
-// One persistent kernel per register class, kEW waves per workgroup (one per SIMD), elastic
-// teams for the batch tail (see Elastic above).  Each wave drains the larger bin first, then the
-// smaller one, exactly as solve_group_kernel.
-template <int NCA, int NCB>
-__global__ void __launch_bounds__(64 * kEW, Cfg<NCA>::WPE)
-    solve_elastic_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
-                         const int* __restrict__ list_b, const int* __restrict__ counts,
-                         int* __restrict__ heads, int qa, float* __restrict__ work,
-                         size_t slab) {
-  static_assert(Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
-  constexpr size_t kR0 = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
-                                                                : sizeof(Smem<NCB>);
-  constexpr int kR = (int)((kR0 + 15) & ~size_t(15));
-  static_assert(sizeof(TeamSmem<NCA, kEW>) <= (size_t)kR && sizeof(TeamSmem<NCB, kEW>) <= (size_t)kR,
-                "a team block fits an idle wave's instance image");
-  __shared__ __attribute__((aligned(16))) unsigned char raw[kEW * kR];
-  __shared__ ElasticCtl ctl;
-  const int wv = uniform((int)(threadIdx.x >> 6));
-  if (threadIdx.x == 0) {
-    ctl.idle = 0;
-    ctl.leader = -1;
-    ctl.nc = 0;
-  }
-  __syncthreads();
-  float* park0 = work + (size_t)blockIdx.x * kEW * slab;
-  float* park = park0 + (size_t)wv * slab;
-  int seq = 0;
-  bool team = false;
-  const Elastic el{&ctl, raw, kR, wv, &seq, &team};
-  unsigned char* mine = raw + wv * kR;
-#ifdef CMPC_STAMPS
-  Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(mine);
-  if ((threadIdx.x & 63) < 32) s0.st[threadIdx.x & 63] = 0;
-#endif
-  drain_bin<NCA, 1>(*reinterpret_cast<Smem<NCA>*>(mine), P, in, out, list_a, counts + qa,
-                    heads + qa, park, nullptr, nullptr, &el);
-  drain_bin<NCB, 1>(*reinterpret_cast<Smem<NCB>*>(mine), P, in, out, list_b, counts + qa - 1,
-                    heads + qa - 1, park, nullptr, nullptr, &el);
-#ifdef CMPC_STAMPS
-  WSYNC();
-  if ((threadIdx.x & 63) < 32) atomicAdd(&g_stamps[threadIdx.x & 63], s0.st[threadIdx.x & 63]);
-#endif
-  elastic_finish<NCA, NCB>(el, P, park0, slab);
 }
 
 // Team mode (cmpc_team.hip): one workgroup of W waves per QP, one kernel for all four bins
@@ -2494,6 +2313,66 @@ __global__ void __launch_bounds__(64 * W, 2)
 #ifdef CMPC_STAMPS
   __syncthreads();
   if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s1.st[threadIdx.x]);
+#endif
+}
+
+// Large batches: ONE kernel for all four bins, a workgroup of two waves (two such waves per SIMD,
+// four workgroups per CU: 256 VGPRs and <= 40 KB of LDS each).
+//  * The NC >= 160 bins first (heaviest first), each QP on the PAIR as a team (cmpc_team.hip,
+//    W = 2): half the tiles per wave, 33 / 39 tiles instead of 55 / 78, so these QPs run two waves
+//    per SIMD instead of one wave alone on a SIMD with its registers spilled.
+//  * Then the NC <= 128 bins, each wave on its own instances (one wave per QP, every tile in its
+//    registers), in its own half of the workgroup's LDS.
+// One register class for every bin: light instances fill the SIMDs that heavy ones leave at the
+// end of the batch, and one launch on the caller's stream replaces the two-stream fork/join.
+// IPM: the light bins carry the interior-point fallback (tail-bound batches).
+constexpr size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
+constexpr size_t kPairOne = align16(sizeof(Smem<128>));          // one light wave's image
+constexpr size_t kPairHeavy = align16(sizeof(Smem<192>));        // the team's instance image
+constexpr size_t kPairTeam = sizeof(TeamSmem<192, 2>);           // the team block
+constexpr size_t kPairBytes = (2 * kPairOne > kPairHeavy + kPairTeam) ? 2 * kPairOne
+                                                                        : kPairHeavy + kPairTeam;
+static_assert(sizeof(Smem<128>) >= sizeof(Smem<96>) && sizeof(Smem<192>) >= sizeof(Smem<160>) &&
+                  sizeof(TeamSmem<192, 2>) >= sizeof(TeamSmem<160, 2>), "images grow with NC");
+// the team block lies past wave 0's light image: the helper reads the closing kOpExit command
+// while the leader may already have started its light instances
+static_assert(kPairHeavy >= kPairOne, "team block clear of wave 0's light image");
+static_assert(kPairBytes <= 40960, "four two-wave workgroups per CU");
+
+template <bool IPM>
+__global__ void __launch_bounds__(128, 2)
+    solve_pair_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ lists,
+                      int64_t stride, const int* __restrict__ counts, int* __restrict__ heads,
+                      float* __restrict__ work, size_t slab, size_t wave_slab) {
+  __shared__ __attribute__((aligned(16))) unsigned char raw[kPairBytes];
+  float* park = work + (size_t)blockIdx.x * slab;
+  const int w = uniform((int)(threadIdx.x >> 6));
+#ifdef CMPC_STAMPS
+  if ((threadIdx.x & 63) < 32) reinterpret_cast<Smem<128>*>(raw + w * kPairOne)->st[threadIdx.x & 63] = 0;
+#endif
+  {
+    Smem<192>& s3 = *reinterpret_cast<Smem<192>*>(raw);
+    Smem<160>& s2 = *reinterpret_cast<Smem<160>*>(raw);
+    TeamSmem<192, 2>& t3 = *reinterpret_cast<TeamSmem<192, 2>*>(raw + kPairHeavy);
+    TeamSmem<160, 2>& t2 = *reinterpret_cast<TeamSmem<160, 2>*>(raw + kPairHeavy);
+    int seq = 0;
+    if (w == 0) {
+      drain_bin<192, 2>(s3, P, in, out, lists + 3 * stride, counts + 3, heads + 3, park, &t3, &seq);
+      drain_bin<160, 2>(s2, P, in, out, lists + 2 * stride, counts + 2, heads + 2, park, &t2, &seq);
+    } else {
+      team_helper<192, 2, 1>(s3, t3, P, park, seq);
+      team_helper<160, 2, 1>(s2, t2, P, park, seq);
+    }
+  }
+  unsigned char* mine = raw + w * kPairOne;
+  float* wpark = park + (size_t)w * wave_slab;
+  drain_bin<128, 1, IPM>(*reinterpret_cast<Smem<128>*>(mine), P, in, out, lists + stride, counts + 1,
+                         heads + 1, wpark);
+  drain_bin<96, 1, IPM>(*reinterpret_cast<Smem<96>*>(mine), P, in, out, lists, counts, heads, wpark);
+#ifdef CMPC_STAMPS
+  WSYNC();
+  if ((threadIdx.x & 63) < 32)
+    atomicAdd(&g_stamps[threadIdx.x & 63], reinterpret_cast<Smem<128>*>(mine)->st[threadIdx.x & 63]);
 #endif
 }
 

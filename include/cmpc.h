@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 2
+#define CMPC_ABI_VERSION 3
 
 #define CMPC_OK 0
 #define CMPC_E_INVALID (-22)   /* bad argument / parameter (EINVAL) */
@@ -80,6 +80,16 @@ typedef struct cmpc_params {
   int32_t ipm_facts;      /* an instance that has failed a polish session and spent this many
                              factorizations identifies its face set by interior-point steps
                              (hard instances); 0 = never.  Default 8 */
+  int32_t check_termination; /* ADMM iterations between termination tests (OPTS check_termination,
+                             centroidal_mpc.py:31): the polish trigger (face set stable for
+                             polish_stable iterations -> active-set polish + KKT check, the only
+                             way an instance ends solved) is evaluated only at iterations that
+                             are multiples of it.  Default 1: here the test is one wave ballot
+                             of the face codes, so checking every iteration costs nothing, while
+                             OSQP's 10 amortises a residual evaluation (two sparse matvecs) this
+                             solver does not need.  The reference's 10 is accepted (the drop-in
+                             CentroidalMPC passes it): same solutions, iterations rounded up to
+                             multiples of 10. */
   int64_t max_batch;      /* largest B passed to cmpc_solve (sizes plan workspace) */
 } cmpc_params;
 
@@ -228,16 +238,21 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
                   const float* force, int64_t force_stride, const float* hip, float* x,
                   float* feet, uint8_t* contact_state, void* stream);
 
-/* Measurement hooks (not on the reference's interface; used by bench.py).  A solve runs two
- * persistent kernels, one per register class: kernel 0 serves the free-variable bins NC 128 and
- * 96 on `stream`, kernel 1 the bins NC 192 and 160 on one plan-internal stream forked from and
- * joined back to `stream` (the two overlap).  While enabled, cmpc_solve records a hipEvent pair
- * around each kernel launch on its own stream; cmpc_plan_timing_read waits for the recorded
- * events, returns the summed milliseconds per kernel (ms_per_kernel[CMPC_NUM_SOLVE_KERNELS]) and
- * launch counts since the last read, and resets them.  At most 4096 solve calls are recorded
- * between reads. */
+/* Measurement hooks (not on the reference's interface; used by bench.py).  A solve launches at
+ * most CMPC_NUM_SOLVE_KERNELS persistent solve kernels; cmpc_plan_solve_kernel names solve
+ * kernel k (0 or 1) of a batch of B instances, or returns NULL if that slot is not launched:
+ *   B <= cmpc_plan_team_batch:  "solve_team_kernel<4>" (k = 0 only);
+ *   larger batches:             "solve_pair_kernel<IPM>" (k = 0 only; IPM = true for
+ *                               B <= cmpc_plan_ipm_batch), every bin in one launch on `stream`.
+ * While enabled, cmpc_solve records a hipEvent pair around each solve-kernel launch on the
+ * stream it is launched on; cmpc_plan_timing_read waits for the recorded events, returns the
+ * summed milliseconds per kernel slot (ms_per_kernel[CMPC_NUM_SOLVE_KERNELS]) and the launch
+ * counts since the last read, and resets them.  At most 4096 x CMPC_NUM_SOLVE_KERNELS launches
+ * are recorded between reads (later ones are not timed). */
 #define CMPC_NUM_SOLVE_KERNELS 2
 int cmpc_plan_set_timing(cmpc_plan* plan, int enable);
+int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_kernel, int32_t* calls_per_kernel);
+const char* cmpc_plan_solve_kernel(const cmpc_plan* plan, int64_t B, int k);
 
 /* Small-batch mode.  A solve of B <= max_batch instances runs each QP on a workgroup of four
  * waves (one per SIMD of a CU) that split the condensation, the inversion and the matrix-vector
@@ -256,7 +271,6 @@ int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
  * B <= 64 x CUs; 0 never.  cmpc_plan_ipm_batch returns the effective bound. */
 int cmpc_plan_set_ipm(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_ipm_batch(const cmpc_plan* plan, int64_t* max_batch);
-int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_kernel, int32_t* calls_per_kernel);
 
 /* Thread-local description of the last error returned on this thread ("" if none). */
 const char* cmpc_last_error(void);

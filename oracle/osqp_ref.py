@@ -101,4 +101,14 @@ def time_baseline(batch: dict, seconds: float = 15.0):
                       f"algorithm restated, reference OPTS, cold start, float64), OpenMP x{cores}",
             "single_thread_ms": per1 * 1e3,
             "osqp_solved_frac": float(np.mean(r["status"] == 1)),
-            "osqp_iters_mean": float(np.mean(r["iters"]))}
+            "osqp_iters_mean": float(np.mean(r["iters"])),
+            "_w": r["w"]}   # the sample's solutions (instances 0 .. n-1), not printed
+
+
+def tight_settings() -> Settings:
+    """The same restatement run to eps 1e-10: it converges to the KKT-certified optimum
+    (tests/test_osqp_port.py), so it measures how far the reference OPTS stop from it."""
+    s = default_settings()
+    s.eps_abs = s.eps_rel = 1e-10
+    s.max_iter = 400000
+    return s

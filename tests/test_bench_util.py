@@ -20,3 +20,46 @@ def test_counters_lookup_ignores_template_flag():
         assert bench._counters_of(c, "solve_group_kernel<192, 160>") is rec_b
         assert bench._counters_of(c, "solve_team_kernel<4>") is None
     assert bench._counters_of(None, "solve_group_kernel<128, 96>") is None
+
+
+class _StubPlan:
+    def __init__(self, names):
+        self.names = names
+
+    def solve_kernels(self, B):
+        return list(self.names)
+
+
+def _batch(n_light, n_heavy, N=16):
+    import numpy as np
+    c = np.zeros((n_light + n_heavy, 4, N), np.uint8)
+    c[:n_light, :, :10] = 1          # 40 stance legs: 120 free forces (NC 128 bin)
+    c[n_light:] = 1                  # 64 stance legs: 192 free forces (NC 192 bin)
+    return c, np.full(n_light + n_heavy, 8, np.int32)
+
+
+def test_roofline_dominant_and_critical_kernels():
+    """Two class kernels: the dominant one processes the most solves, the critical one has the
+    longest live time (it sets the step); the HBM fraction is algorithmic bytes / live time."""
+    contact, iters = _batch(900, 100)
+    bins = bench.bins_of(contact)
+    plan = _StubPlan(["solve_group_kernel<128, 96, false>", "solve_group_kernel<192, 160, false>"])
+    roof, comp, crit = bench.kernel_roofline(plan, 1000, bins, contact, iters, [9.0, 12.0], [1, 1],
+                                             step_ms=12.5)
+    assert roof["kernel"].startswith("solve_group_kernel<128") and roof["solves_per_launch"] == 900
+    assert crit["kernel"].startswith("solve_group_kernel<192") and crit["solves_per_launch"] == 100
+    assert not crit["same_as_dominant"] and abs(crit["step_share"] - 12.0 / 12.5) < 1e-12
+    assert abs(roof["achieved"] - bench.BYTES_PER_SOLVE * 900 / 9e-3 / 1e9) < 1e-9
+    assert abs(crit["frac"] - bench.BYTES_PER_SOLVE * 100 / 12e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-12
+    assert comp["kernel"] == roof["kernel"] and crit["compute"]["kernel"] == crit["kernel"]
+
+
+def test_roofline_single_kernel():
+    """One solve kernel for every bin (pair kernel): dominant == critical, all solves counted."""
+    contact, iters = _batch(900, 100)
+    plan = _StubPlan(["solve_pair_kernel<false>", None])
+    roof, comp, crit = bench.kernel_roofline(plan, 1000, bench.bins_of(contact), contact, iters,
+                                             [10.0, 0.0], [2, 0], step_ms=5.2)
+    assert roof["kernel"] == crit["kernel"] == "solve_pair_kernel<false>"
+    assert roof["solves_per_launch"] == 1000 and roof["kernel_avg_ms"] == 5.0
+    assert crit["same_as_dominant"] and list(roof["kernel_avg_ms_all"]) == ["solve_pair_kernel<false>"]

@@ -42,13 +42,15 @@ def test_defaults_are_reference_constants(lib):
     assert abs(p.eps_abs - 1e-4) < 1e-9 and p.max_iter == 1000           # :25-27
     assert p.adaptive_rho_interval == 25                                 # :32
     assert p.ipm_facts == 8  # interior-point fallback for hard instances
-    assert ctypes.sizeof(_lib.CParams) == 168  # include/cmpc.h layout (int64 max_batch at 160)
+    assert p.check_termination == 1  # OPTS check_termination (:31 has 10; include/cmpc.h says why)
+    assert ctypes.sizeof(_lib.CParams) == 176  # include/cmpc.h layout (int64 max_batch at 168)
+    assert _lib.CParams.max_batch.offset == 168
     assert lib.cmpc_version().decode().startswith("cmpc 1")
 
 
 @pytest.mark.parametrize("field,value", [("N", 0), ("N", 17), ("mu", -1.0), ("max_iter", 0),
                                          ("alpha", 2.5), ("rho", 0.0), ("max_batch", 0),
-                                         ("ipm_facts", -1)])
+                                         ("ipm_facts", -1), ("check_termination", 0)])
 def test_invalid_params_rejected_before_device(lib, field, value):
     from cmpc import _lib
     p = _lib.CParams()

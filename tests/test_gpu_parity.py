@@ -153,3 +153,20 @@ def test_full_size_certified_sample(plan):
     err = rel_err_U(w[idx], fx["w"])
     worst = int(err.argmax())
     assert err.max() <= TOL_U, (err.max(), int(idx[worst]), int(fx["bins"][worst]))
+
+
+def test_check_termination_reference_interval():
+    """OPTS check_termination = 10 (centroidal_mpc.py:31, cmpc_params.check_termination): the
+    termination test (polish trigger) runs only every 10th ADMM iteration.  Same solutions within
+    the parity bar; every cold solve ends at a multiple of 10 iterations.  Both the small-batch
+    (team) and the large-batch path."""
+    from cmpc import Plan, SolverParams, solve_batch
+    fx = load_fixture("qp_cfg2.npz")
+    plan10 = Plan(SolverParams(max_batch=4096, check_termination=10))
+    for reps in (1, 40):
+        batch = {k: np.repeat(v, reps, axis=0) for k, v in fixture_batch(fx).items()}
+        w, st, it = solve_batch(batch, plan=plan10)
+        assert np.all(st == 1), np.unique(st, return_counts=True)
+        assert np.all(it % 10 == 0) and it.min() >= 10, np.unique(it)
+        err = rel_err_U(w, np.repeat(fx["w"], reps, axis=0))
+        assert err.max() <= TOL_U, err.max()

@@ -20,7 +20,9 @@ def main():
     _lib._lib = _lib.load(lib)
     from cmpc import Plan, SolverParams, to_device_batch, synth
     plan = Plan(SolverParams(max_batch=65536))
-    for cfg, B in ((3, 8192), (2, 4096), (3, 16384), (3, 65536)):
+    cases = [(int(c), int(b)) for c, b in (a.split(":") for a in sys.argv[2:])] or \
+        [(3, 8192), (2, 4096), (3, 16384), (3, 65536)]
+    for cfg, B in cases:
         b = synth.make_config(cfg, B)
         d = to_device_batch(b)
         nc = 3 * (b["contact"].reshape(B, -1) != 0).sum(1)
@@ -41,6 +43,13 @@ def main():
                 print(f"  {name}: {m.sum()} inst, last end {t1[m].max() / 100:.0f} us, "
                       f"p50 end {np.percentile(t1[m], 50) / 100:.0f} us, mean dur {dur[m].mean() / 100:.1f} us, "
                       f"last start {t0[m].max() / 100:.0f} us")
+        # concurrency: instances in flight of each class at 12 points of the batch (in group
+        # mode the heavy count is the number of SIMDs the one-wave heavy class holds)
+        pts = np.linspace(0, end, 14)[1:-1]
+        for name, m in (("light", ~heavy), ("heavy", heavy)):
+            if m.any():
+                act = [int(np.sum(m & (t0 <= p) & (t1 > p))) for p in pts]
+                print(f"  {name} in flight: " + " ".join(f"{a:5d}" for a in act))
         order = np.argsort(-t1)[:8]
         for i in order:
             print(f"    inst {i:6d} {'heavy' if heavy[i] else 'light'} nc {nc[i]:3d} start {t0[i] / 100:7.0f} us "
