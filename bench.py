@@ -129,11 +129,12 @@ def parse(argv=None):
                     help="0 = headline only (profiling runs): skips every other object")
     ap.add_argument("--seed-offset", type=int, default=0,
                     help="added to the workload seed (experiments: average over batches)")
-    ap.add_argument("--param", action="append", default=[],
-                    help="SolverParams override key=value (experiments)")
+    ap.add_argument("--param", action="append",
+                    default=[kv for kv in os.environ.get("CMPC_PARAMS", "").split(",") if kv],
+                    help="SolverParams override key=value (experiments; also $CMPC_PARAMS k=v,k=v)")
     ap.add_argument("--team", type=int, default=-1,
                     help="small-batch team mode for B <= this (cmpc_plan_set_team): -1 auto, 0 off")
-    ap.add_argument("--ipm", type=int, default=-1,
+    ap.add_argument("--ipm", type=int, default=int(os.environ.get("CMPC_IPM_BATCH", "-1")),
                     help="interior-point fallback kernels for B <= this (cmpc_plan_set_ipm): -1 auto")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")

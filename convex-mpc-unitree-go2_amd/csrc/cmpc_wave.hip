@@ -362,8 +362,8 @@ constexpr int kSweepPipeMaxNC = CMPC_SWEEP_PIPE_MAX_NC;
 // Each step issues its MFMAs on those tiles first, publishes the next panel from them, and then
 // issues the remaining MFMAs of the step in the same basic block as the next step's LDL and
 // operand build, so that serial chain fills the gaps between MFMAs instead of stalling the wave.
-template <int NC, int K>
-__device__ __forceinline__ void sweep_publish(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], int sub,
+template <int NC, int K, class SM>
+__device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL], int sub,
                                               int g, int c) {
   using C = Cfg<NC>;
   const int c0 = 4 * sub;
@@ -389,8 +389,8 @@ __device__ __forceinline__ void sweep_publish(Smem<NC>& s, const f4 (&M)[Cfg<NC>
 }
 
 // LDL of the 4x4 pivot block (rows k0..k0+3 of the panel) and the step's MFMA operands
-template <int NC>
-__device__ __forceinline__ void sweep_operands(Smem<NC>& s, int k0, int g, int c,
+template <int NC, class SM>
+__device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
                                                float (&a)[Cfg<NC>::TT], float (&b)[Cfg<NC>::TT]) {
   using C = Cfg<NC>;
   const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
@@ -456,8 +456,8 @@ __device__ __forceinline__ void sweep_diagfix(f4 (&M)[Cfg<NC>::NTL], int sub, in
   for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
 }
 
-template <int NC, int K>
-__device__ __forceinline__ void sweep_block(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL], int ng, int TA,
+template <int NC, int K, class SM>
+__device__ __forceinline__ void sweep_block(SM& s, f4 (&M)[Cfg<NC>::NTL], int ng, int TA,
                                             int g, int c, float (&a)[Cfg<NC>::TT],
                                             float (&b)[Cfg<NC>::TT]) {
   using C = Cfg<NC>;
@@ -654,8 +654,8 @@ __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
 // ------------------------------------------------------------------------------------------
 // block sweep inversion (4 pivots per step, MFMA rank-4 updates)
 // ------------------------------------------------------------------------------------------
-template <int NC>
-__device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL], int n) {
+template <int NC, class SM>
+__device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n) {
   using C = Cfg<NC>;
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
@@ -801,8 +801,8 @@ __device__ __forceinline__ void invert_tiles(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL],
 
 // out = M in over the first n params (M in register tiles, symmetric, lower triangle stored);
 // `in` is read (and treated as zero) beyond n, out is zero there
-template <int NC>
-__device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], int n,
+template <int NC, class SM>
+__device__ __forceinline__ void symv(SM& s, const f4 (&M)[Cfg<NC>::NTL], int n,
                                      const float* in, float* out) {
   using C = Cfg<NC>;
   CMPC_T0(t_sv);
@@ -873,8 +873,8 @@ __device__ __forceinline__ void symv(Smem<NC>& s, const f4 (&M)[Cfg<NC>::NTL], i
 // is the trajectory itself).  A^d and (A')^d come from repeated squaring in the same layout.
 // powers A^d and (A')^d, d = 1, 2, 4, 8, in accumulator layout over state positions
 // (pw[l][q] = A^(2^l)[state 3g+q][state of position c]); the gradient's scans use them
-template <int NC>
-__device__ __forceinline__ void gradient_powers(Smem<NC>& s, f4 (&pw)[4], f4 (&tw)[4]) {
+template <class SM>
+__device__ __forceinline__ void gradient_powers(SM& s, f4 (&pw)[4], f4 (&tw)[4]) {
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
   const int sc = ((c & 3) < 3) ? 3 * (c >> 2) + (c & 3) : -1;
@@ -958,7 +958,7 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
       tw[l] = twc[l];
     }
   } else {
-    gradient_powers<NC>(s, pw, tw);
+    gradient_powers(s, pw, tw);
   }
   // forward scan: E[:, k] += A^d E[:, k - d]  (A operand = (A^d)' = tw)
 #pragma unroll
@@ -1716,7 +1716,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   // (NC <= 128 only: the larger bins need those registers for their tiles)
   constexpr bool kPow = W > 1 && NC <= 128;
   f4 pw_c[4], tw_c[4];
-  if constexpr (kPow) gradient_powers<NC>(s, pw_c, tw_c);
+  if constexpr (kPow) gradient_powers(s, pw_c, tw_c);
   const f4* pwc = kPow ? pw_c : nullptr;
   const f4* twc = kPow ? tw_c : nullptr;
   // initial rho per bin: the NC = 128 bin (33-42 stance triples, trot-like schedules) converges
@@ -2316,66 +2316,6 @@ __global__ void __launch_bounds__(64 * W, 2)
 #endif
 }
 
-// Large batches: ONE kernel for all four bins, a workgroup of two waves (two such waves per SIMD,
-// four workgroups per CU: 256 VGPRs and <= 40 KB of LDS each).
-//  * The NC >= 160 bins first (heaviest first), each QP on the PAIR as a team (cmpc_team.hip,
-//    W = 2): half the tiles per wave, 33 / 39 tiles instead of 55 / 78, so these QPs run two waves
-//    per SIMD instead of one wave alone on a SIMD with its registers spilled.
-//  * Then the NC <= 128 bins, each wave on its own instances (one wave per QP, every tile in its
-//    registers), in its own half of the workgroup's LDS.
-// One register class for every bin: light instances fill the SIMDs that heavy ones leave at the
-// end of the batch, and one launch on the caller's stream replaces the two-stream fork/join.
-// IPM: the light bins carry the interior-point fallback (tail-bound batches).
-constexpr size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
-constexpr size_t kPairOne = align16(sizeof(Smem<128>));          // one light wave's image
-constexpr size_t kPairHeavy = align16(sizeof(Smem<192>));        // the team's instance image
-constexpr size_t kPairTeam = sizeof(TeamSmem<192, 2>);           // the team block
-constexpr size_t kPairBytes = (2 * kPairOne > kPairHeavy + kPairTeam) ? 2 * kPairOne
-                                                                        : kPairHeavy + kPairTeam;
-static_assert(sizeof(Smem<128>) >= sizeof(Smem<96>) && sizeof(Smem<192>) >= sizeof(Smem<160>) &&
-                  sizeof(TeamSmem<192, 2>) >= sizeof(TeamSmem<160, 2>), "images grow with NC");
-// the team block lies past wave 0's light image: the helper reads the closing kOpExit command
-// while the leader may already have started its light instances
-static_assert(kPairHeavy >= kPairOne, "team block clear of wave 0's light image");
-static_assert(kPairBytes <= 40960, "four two-wave workgroups per CU");
-
-template <bool IPM>
-__global__ void __launch_bounds__(128, 2)
-    solve_pair_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ lists,
-                      int64_t stride, const int* __restrict__ counts, int* __restrict__ heads,
-                      float* __restrict__ work, size_t slab, size_t wave_slab) {
-  __shared__ __attribute__((aligned(16))) unsigned char raw[kPairBytes];
-  float* park = work + (size_t)blockIdx.x * slab;
-  const int w = uniform((int)(threadIdx.x >> 6));
-#ifdef CMPC_STAMPS
-  if ((threadIdx.x & 63) < 32) reinterpret_cast<Smem<128>*>(raw + w * kPairOne)->st[threadIdx.x & 63] = 0;
-#endif
-  {
-    Smem<192>& s3 = *reinterpret_cast<Smem<192>*>(raw);
-    Smem<160>& s2 = *reinterpret_cast<Smem<160>*>(raw);
-    TeamSmem<192, 2>& t3 = *reinterpret_cast<TeamSmem<192, 2>*>(raw + kPairHeavy);
-    TeamSmem<160, 2>& t2 = *reinterpret_cast<TeamSmem<160, 2>*>(raw + kPairHeavy);
-    int seq = 0;
-    if (w == 0) {
-      drain_bin<192, 2>(s3, P, in, out, lists + 3 * stride, counts + 3, heads + 3, park, &t3, &seq);
-      drain_bin<160, 2>(s2, P, in, out, lists + 2 * stride, counts + 2, heads + 2, park, &t2, &seq);
-    } else {
-      team_helper<192, 2, 1>(s3, t3, P, park, seq);
-      team_helper<160, 2, 1>(s2, t2, P, park, seq);
-    }
-  }
-  unsigned char* mine = raw + w * kPairOne;
-  float* wpark = park + (size_t)w * wave_slab;
-  drain_bin<128, 1, IPM>(*reinterpret_cast<Smem<128>*>(mine), P, in, out, lists + stride, counts + 1,
-                         heads + 1, wpark);
-  drain_bin<96, 1, IPM>(*reinterpret_cast<Smem<96>*>(mine), P, in, out, lists, counts, heads, wpark);
-#ifdef CMPC_STAMPS
-  WSYNC();
-  if ((threadIdx.x & 63) < 32)
-    atomicAdd(&g_stamps[threadIdx.x & 63], reinterpret_cast<Smem<128>*>(mine)->st[threadIdx.x & 63]);
-#endif
-}
-
 // Binning of a small batch (B <= 1024) in one workgroup: counts are written, not accumulated,
 // and the queue heads are zeroed here, so no memset precedes it (one launch less per solve).
 __global__ void __launch_bounds__(1024) bin_small_kernel(int N, int B,
@@ -2457,5 +2397,7 @@ __global__ void __launch_bounds__(256) bin_kernel(int N, int64_t B,
     }
   }
 }
+
+#include "cmpc_wspace.hip"  // large batches: the wrench-space factorization, one kernel
 
 }  // namespace cmpc

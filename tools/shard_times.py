@@ -24,6 +24,8 @@ def main():
     # IPM_FACTS: the interior-point trigger (SolverParams.ipm_facts) for trigger sweeps
     facts = int(os.environ.get("IPM_FACTS", SolverParams.ipm_facts))
     plan = Plan(SolverParams(max_batch=65536, ipm_facts=facts))
+    if os.environ.get("CMPC_IPM_BATCH"):  # kernel variants with the fallback up to this batch
+        plan.set_ipm(int(os.environ["CMPC_IPM_BATCH"]))
     d = to_device_batch(synth.make_config(3))
     B = d["Ad"].shape[0]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
