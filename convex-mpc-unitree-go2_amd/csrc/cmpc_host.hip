@@ -26,7 +26,7 @@ struct cmpc_plan {
   cmpc::KParams kp;
   int device;
   int cus = 0;      // compute units of the device
-  int* d_counters;  // counts[kNumBins], heads[kNumBins], the wrench-space queue head
+  int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
   float* d_work;    // per-wave park slabs; group k's region starts at work_off[k] (groups overlap)
   size_t work_off[kNumGroups];
@@ -40,12 +40,6 @@ struct cmpc_plan {
   // tail-bound batches (B <= ipm_max_batch): the one-wave kernel variants with the
   // interior-point fallback for hard instances
   int64_t ipm_max_batch = -1;   // -1: automatic (B <= 64 x CUs)
-  // large batches: the wrench-space kernel for every instance (cmpc_wspace.hip solve_ws_kernel;
-  // instances whose Bd is not of the centroidal form go on to the n-space kernels), or the
-  // n-space register-class kernels on two streams (solve_group_kernel)
-  bool ws = false;
-  int ws_grid = 0;
-  size_t ws_off = 0;          // its slabs in d_work
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
   // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
   // stream forked from / joined to it.  Two streams in total stay within the device's hardware
@@ -214,23 +208,6 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   }
   {
     int nb = 0;
-    nb = 1 << 30;
-    for (int v = 0; v < 2; ++v) {
-      int b = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, v ? cmpc::solve_ws_kernel<true> : cmpc::solve_ws_kernel<false>, 64, 0);
-      if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
-      nb = std::min(nb, b);
-    }
-    if (nb < 1) { delete pl; return fail(CMPC_E_HIP, "cmpc_plan_create: solve_ws_kernel cannot be resident"); }
-    pl->ws_grid = nb * cus;
-    // the wrench-space kernel's slabs follow the n-space kernels' (its fallback runs after it)
-    pl->ws_off = work_floats;
-    work_floats += (size_t)pl->ws_grid * cmpc::kWsSlab;
-    // (experiment, not adopted: CMPC_SOLVE_KERNEL=ws solves large batches in the wrench space)
-    if (const char* m = getenv("CMPC_SOLVE_KERNEL")) pl->ws = strcmp(m, "ws") == 0;
-  }
-  {
-    int nb = 0;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc::solve_team_kernel<kTeamWaves>,
                                                      64 * kTeamWaves, 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
@@ -240,7 +217,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
                               cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB});
     work_floats = std::max(work_floats, (size_t)pl->team_grid * pl->team_slab);
   }
-  e = hipMalloc(&pl->d_counters, (2 * cmpc::kNumBins + 1) * sizeof(int));
+  e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
   e = hipMalloc(&pl->d_work, work_floats * sizeof(float));
   if (e != hipSuccess) {
@@ -380,51 +357,6 @@ static int record_team_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams&
   return CMPC_OK;
 }
 
-// large batches: every instance in one launch of the wrench-space kernel (timed as kernel 0); the
-// n-space kernels then drain the bins of instances it handed on (normally none: they exit at once)
-static int record_ws_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams& kp,
-                            const cmpc::Inputs& in, const cmpc::Outputs& out, int64_t B, bool ipm) {
-  hipError_t e;
-  cmpc_plan::Rec rec{nullptr, nullptr, 0};
-  const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
-  if (rec_this) {
-    if (!pl->pool.empty()) {
-      rec = pl->pool.back();
-      pl->pool.pop_back();
-      rec.group = 0;
-    } else {
-      if ((e = hipEventCreate(&rec.a)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-      if ((e = hipEventCreate(&rec.b)) != hipSuccess) return hip_fail(e, "hipEventCreate");
-    }
-    if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-  }
-  const unsigned g = (unsigned)(pl->ws_grid < B ? pl->ws_grid : B);
-  const cmpc::Fallback fb{pl->d_counters, pl->d_lists, (int64_t)pl->p.max_batch};
-  hipLaunchKernelGGL(ipm ? cmpc::solve_ws_kernel<true> : cmpc::solve_ws_kernel<false>, dim3(g),
-                     dim3(64), 0, s, kp, in, out, B,
-                     pl->d_counters + 2 * cmpc::kNumBins, fb, pl->d_work + pl->ws_off);
-  e = hipGetLastError();
-  if (e != hipSuccess) return hip_fail(e, "solve_ws_kernel launch");
-  if (rec_this) {
-    if ((e = hipEventRecord(rec.b, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
-    pl->recs.push_back(rec);
-  }
-  // the handed-on instances, by the n-space kernels of their register class (one after the
-  // other on `s`: normally both find empty bins and exit at once)
-  for (int k = 1; k >= 0; --k) {
-    const int qa = group_first_bin(k);
-    const unsigned gk = (unsigned)(pl->grid[k] < B ? pl->grid[k] : B);
-    hipLaunchKernelGGL(group_fn(k, ipm), dim3(gk), dim3(64), 0, s, kp, in, out,
-                       pl->d_lists + (size_t)qa * pl->p.max_batch,
-                       pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
-                       pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
-                       pl->slab[k]);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "solve_group_kernel (fallback) launch");
-  }
-  return CMPC_OK;
-}
-
 static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cmpc::Outputs& out,
                       void* stream) {
   int rc = check_device(pl, "cmpc_solve");
@@ -434,13 +366,8 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   cmpc::KParams kp = pl->kp;
   // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
-  // tail-bound batch: the n-space kernel variants with the interior-point fallback
+  // tail-bound batch: the kernel variants with the interior-point fallback
   const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
-  if (pl->ws && B > team_batch(pl)) {  // every instance through the wrench-space kernel
-    e = hipMemsetAsync(pl->d_counters, 0, (2 * cmpc::kNumBins + 1) * sizeof(int), st);
-    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-    return record_ws_launch(pl, st, kp, in, out, B, ipm);
-  }
   if (B <= 1024) {  // one workgroup bins the batch and zeroes the queue heads (no memset)
     hipLaunchKernelGGL(cmpc::bin_small_kernel, dim3(1), dim3(1024), 0, st, pl->kp.N, (int)B,
                        in.contact, pl->d_counters, pl->d_counters + cmpc::kNumBins, pl->d_lists,
@@ -613,7 +540,6 @@ const char* cmpc_plan_solve_kernel(const cmpc_plan* pl, int64_t B, int k) {
   if (!pl || B < 1 || k < 0 || k >= kNumGroups) return nullptr;
   if (B <= team_batch(pl)) return k == 0 ? "solve_team_kernel<4>" : nullptr;
   const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
-  if (pl->ws) return k == 0 ? (ipm ? "solve_ws_kernel<true>" : "solve_ws_kernel<false>") : nullptr;
   if (k == 1 && !(cmpc::kBinCap[1] < 12 * pl->kp.N)) return nullptr;
   if (k == 0) return ipm ? "solve_group_kernel<128, 96, true>" : "solve_group_kernel<128, 96, false>";
   return ipm ? "solve_group_kernel<192, 160, true>" : "solve_group_kernel<192, 160, false>";

@@ -2398,6 +2398,4 @@ __global__ void __launch_bounds__(256) bin_kernel(int N, int64_t B,
   }
 }
 
-#include "cmpc_wspace.hip"  // large batches: the wrench-space factorization, one kernel
-
 }  // namespace cmpc
