@@ -285,7 +285,7 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
         const int p = 16 * J + c;
         float bt[3];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) bt[q] = s.Bt[p * 12 + 3 * g + q];
+        for (int q = 0; q < 3; ++q) bt[q] = s.Bt[p * kBS + 3 * g + q];
         f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 3; ++q) d = mfma4(Pt[q], (p < n) ? bt[q] : 0.f, d);
@@ -342,7 +342,7 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
           const int J = (pr < T::NPAIR) ? (h ? TT - 1 - pr : pr) : 0;
           bn[j][h] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int q = 0; q < 3; ++q) bn[j][h][q] = s.Bt[(16 * J + c) * 12 + 3 * g + q];
+          for (int q = 0; q < 3; ++q) bn[j][h][q] = s.Bt[(16 * J + c) * kBS + 3 * g + q];
         }
       }
       pin(alo);

@@ -214,13 +214,28 @@ constexpr int kLateRepairs = 3;      // repair budget of the sessions after two 
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
+// After its first failed polish session an instance continues ADMM at kFailRho x rho0.  The
+// slow instances are the ones whose repairs cycle between neighbouring face sets (a degenerate
+// corner of the pyramid: fz at fz_min with friction faces weakly active, coupled over steps);
+// a stiffer rho settles ADMM's face set closer to the optimum's before the next session.  NumPy
+// model (tests/algo_spec.py) over 8,192 config-3 / config-2 instances: mean factorizations
+// unchanged, the slowest instance 30 -> 17 (config 3) and 42 -> 26 (config 2) factorizations.
+#ifndef CMPC_FAIL_RHO
+#define CMPC_FAIL_RHO 4.f
+#endif
+constexpr float kFailRho = CMPC_FAIL_RHO;
+
+// Stride of a param's column in Smem::Bt.  (An odd stride, 13, spreads the gradient's per-step
+// column reads over more LDS banks -- 12 puts the 16 steps' columns of a trot on 4 -- but it
+// loses the 16-byte loads elsewhere: -1..-6 % on every workload, A/B in one gpurun call.)
+constexpr int kBS = 12;
 
 template <int NC>
 struct Smem {
 #ifdef CMPC_STAMPS
   unsigned long long st[32];       // per-wave stamp totals (flushed to g_stamps at exit)
 #endif
-  alignas(16) float Bt[NC * 12];   // param-space input matrix, column p at Bt[12p .. 12p+11]
+  alignas(16) float Bt[NC * kBS];  // param-space input matrix, column p at Bt[kBS p .. kBS p + 11]
   alignas(16) float Rt[NC];        // param-space input weight (2R in the param basis)
   alignas(16) float x[NC];
   alignas(16) float z[NC];
@@ -248,9 +263,9 @@ struct Smem {
   int off[kMaxN + 1];              // first param of step k
   int tri[kMaxTri];                // stance triple t -> 4k + leg
   int tri_of[kMaxTri];             // 4k + leg -> triple index or -1
-  int tcnt[kMaxTri];               // polish: params of triple t / repaired face code
-  int code[kMaxTri];               // face code of triple t
-  int pcode[kMaxTri];              // face code of the previous ADMM iteration
+  int8_t tcnt[kMaxTri];            // polish: params of triple t / repaired face code
+  int8_t code[kMaxTri];            // face code of triple t
+  int8_t pcode[kMaxTri];           // face code of the previous ADMM iteration (-1: none)
   int fpk[kMaxTri];                // polish: params of triple t, px | py << 8 | pz << 16 (255 none)
   uint8_t fpat[kFailMem][kMaxTri]; // starting face sets of failed polish sessions
   uint8_t tpat[kTryMem][kMaxTri];  // face sets tried in the current session (0 = its start)
@@ -314,7 +329,7 @@ __device__ __forceinline__ void condense_tiles_fwd(Smem<NC>& s, const KParams& P
       if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
       const int p = 16 * J + c;
       if (p >= p0 && p < p1) {
-        const float* bp = &s.Bt[p * 12 + 3 * g];
+        const float* bp = &s.Bt[p * kBS + 3 * g];
         Gd[J] = f4{bp[0], bp[1], bp[2], 0.f};
       }
     }
@@ -529,7 +544,7 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
       const int p = 16 * J + c;
       float bt[3];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) bt[q] = (p < n) ? s.Bt[p * 12 + 3 * g + q] : 0.f;
+      for (int q = 0; q < 3; ++q) bt[q] = (p < n) ? s.Bt[p * kBS + 3 * g + q] : 0.f;
       f4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < 3; ++q) d = mfma4(Pt[q], bt[q], d);  // C = P B (P symmetric)
@@ -573,7 +588,7 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
       if (16 * J + 15 < p0 || 16 * J >= p1) continue;  // uniform
       const int p = 16 * J + c;
       if (p >= p0 && p < p1) {
-        const float* bp = &s.Bt[p * 12 + 3 * g];
+        const float* bp = &s.Bt[p * kBS + 3 * g];
         Gd[J] = f4{bp[0], bp[1], bp[2], 0.f};
       }
     }
@@ -927,7 +942,7 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
     for (int i = 0; i < 12; ++i) {
       const int p = min(p0 + i, NC - 1);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) bv[i][q] = s.Bt[p * 12 + 3 * g + q];
+      for (int q = 0; q < 3; ++q) bv[i][q] = s.Bt[p * kBS + 3 * g + q];
       vv[i] = vin[p];
     }
 #pragma unroll
@@ -944,7 +959,7 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
     for (int q = 0; q < 3; ++q) Et[q] = s.Dt[12 * c + 3 * g + q];
     const int p1 = s.off[c + 1];
     for (int p = s.off[c]; p < p1; ++p) {
-      const float* bt = &s.Bt[p * 12 + 3 * g];
+      const float* bt = &s.Bt[p * kBS + 3 * g];
       const float vp = vin[p];
 #pragma unroll
       for (int q = 0; q < 3; ++q) Et[q] = fmaf(bt[q], vp, Et[q]);
@@ -1008,9 +1023,9 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
   WSYNC();
   for (int p = lane; p < n; p += 64) {  // g = B~' lambda + Rt v
     const int k = s.par[p];
-    const f4* bt = reinterpret_cast<const f4*>(&s.Bt[p * 12]);
     const f4* l = reinterpret_cast<const f4*>(&s.L[12 * k]);
     f2 a2 = {s.Rt[p] * vin[p], 0.f};  // packed: even and odd states in the two halves
+    const f4* bt = reinterpret_cast<const f4*>(&s.Bt[p * kBS]);
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const f4 lv = l[j], bv = bt[j];
@@ -1062,7 +1077,7 @@ __device__ __forceinline__ void build_admm_basis(Smem<NC>& s, const KParams& P,
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
 #pragma unroll
-      for (int r = 0; r < 12; ++r) s.Bt[(3 * lane + a) * 12 + r] = bv[3 * r + a];
+      for (int r = 0; r < 12; ++r) s.Bt[(3 * lane + a) * kBS + r] = bv[3 * r + a];
     }
   }
   for (int p = lane; p < NC; p += 64) {
@@ -1126,7 +1141,7 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
     if (sx == 0) {
       px = p++;
 #pragma unroll
-      for (int r = 0; r < 12; ++r) s.Bt[px * 12 + r] = bx[r];
+      for (int r = 0; r < 12; ++r) s.Bt[px * kBS + r] = bx[r];
       s.Rt[px] = s.R2[3 * leg];
       s.par[px] = k;
       s.v[px] = s.z[3 * lane];
@@ -1134,7 +1149,7 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
     if (sy == 0) {
       py = p++;
 #pragma unroll
-      for (int r = 0; r < 12; ++r) s.Bt[py * 12 + r] = by[r];
+      for (int r = 0; r < 12; ++r) s.Bt[py * kBS + r] = by[r];
       s.Rt[py] = s.R2[3 * leg + 1];
       s.par[py] = k;
       s.v[py] = s.z[3 * lane + 1];
@@ -1143,7 +1158,7 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
       pz = p++;
       const float cx = sx * mu, cy = sy * mu;
 #pragma unroll
-      for (int r = 0; r < 12; ++r) s.Bt[pz * 12 + r] = bz[r] + cx * bx[r] + cy * by[r];
+      for (int r = 0; r < 12; ++r) s.Bt[pz * kBS + r] = bz[r] + cx * bx[r] + cy * by[r];
       s.Rt[pz] = s.R2[3 * leg + 2] + mu * mu * ((sx != 0 ? s.R2[3 * leg] : 0.f) +
                                                 (sy != 0 ? s.R2[3 * leg + 1] : 0.f));
       s.par[pz] = k;
@@ -1812,6 +1827,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int nsfail = 0;         // failed sessions, remembered starts included
   int nfact = 0;          // factorizations so far
   bool ipm_session = false;  // the current polish session started from its face set
+  bool fail_rho_done = false;  // rho moved to kFailRho x rho0 after the first failed session
   const float alpha = P.alpha;
   if (n == 0) status = 1;
   if (n > 0 && in.w_init != nullptr) {
@@ -1927,6 +1943,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       if (ipm_session) {  // ADMM resumes from where it was before the interior-point steps
         ipm_session = false;
         ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
+      }
+      // (before the interior-point fallback: that one serves the instances still failing after it)
+      if (nfail == 1 && !seen_start && kFailRho != 1.f && !fail_rho_done) {
+        // the first failed session: a hard instance continues at kFailRho x rho0 (one refactor;
+        // nothing is parked before the second session, so it would refactor anyway)
+        fail_rho_done = true;
+        rho_low = false;
+        rho = uniformf(kFailRho * P.rho0);
+        shift = uniformf(P.sigma + rho);
+        refactor = true;
+        continue;
       }
       if constexpr (W == 1 && IPM && kIpmAfter > 0) {
         if (!ipm_done && P.ipm_facts > 0 && nsfail >= kIpmAfter && nfact >= P.ipm_facts) {

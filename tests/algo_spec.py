@@ -277,7 +277,10 @@ def solve(inst, p: Params):
                 status = 1; U = u; break
             if not seen:
                 failed_starts.append(start)
-            if rho_low:
+            if len(failed_starts) == 1 and not seen:
+                # the first failed session: continue at 4 x rho0 (cmpc_wave.hip kFailRho)
+                rho_low = False; rho = 4.0 * p.rho; L = admm_matrix(rho)
+            elif rho_low:
                 rho_low = False; rho = p.rho; L = admm_matrix(rho)
         if p.adaptive_interval and it % p.adaptive_interval == 0:
             rp = np.max(np.abs(x - z)); rd = np.max(np.abs(g + y))
