@@ -3,6 +3,7 @@
 instance finished in an elastic team).  Shows what sets the end of a batch: the slowest
 instances, when they started, and whether the batch tail ran in team mode."""
 import functools
+import os
 import sys
 from pathlib import Path
 
@@ -27,9 +28,14 @@ def main():
         d = to_device_batch(b)
         nc = 3 * (b["contact"].reshape(B, -1) != 0).sum(1)
         heavy = nc > 128
-        for rep in range(2):
-            w, st, it = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"])
-            torch.cuda.synchronize()
+        # REPS back-to-back solves (as bench.py times them); the last one's timeline is shown
+        w = torch.empty((B, 24 * 16), dtype=torch.float32, device="cuda")
+        st = torch.empty((B,), dtype=torch.int32, device="cuda")
+        it = torch.empty((B,), dtype=torch.int32, device="cuda")
+        for rep in range(int(os.environ.get("REPS", "2"))):
+            plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"], out=(w, st, it),
+                       stream=torch.cuda.current_stream())
+        torch.cuda.synchronize()
         t0 = st.cpu().numpy().astype(np.int64)
         code = it.cpu().numpy().astype(np.int64)
         team = code >= 1000000000
