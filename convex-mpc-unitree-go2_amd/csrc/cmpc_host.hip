@@ -26,10 +26,7 @@ struct cmpc_plan {
   cmpc::KParams kp;
   int device;
   int cus = 0;      // compute units of the device
-  int* d_counters;  // counts[kNumBins], heads[kNumBins], then the racing state (race_off)
-  size_t race_off[kNumGroups];  // each kernel's inflight table (grid ints) within d_counters
-  size_t race_state = 0;        // per-instance racing state (max_batch ints) within d_counters
-  bool race = true;             // straggler racing (cmpc_wave.hip Race); CMPC_RACE=0 turns it off
+  int* d_counters;  // counts[kNumBins], heads[kNumBins]
   int* d_lists;     // kNumBins * max_batch
   float* d_work;    // per-wave park slabs; group k's region starts at work_off[k] (groups overlap)
   size_t work_off[kNumGroups];
@@ -70,7 +67,7 @@ int hip_fail(hipError_t e, const char* what) {
 }
 
 using KernelFn = void (*)(cmpc::KParams, cmpc::Inputs, cmpc::Outputs, const int*, const int*,
-                          const int*, int*, int, float*, size_t, cmpc::Race);
+                          const int*, int*, int, float*, size_t);
 
 // The plan's workspace, streams and events belong to the device current at cmpc_plan_create:
 // every launch must run there (the Python layer makes the tensors' device current).
@@ -220,16 +217,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
                               cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB});
     work_floats = std::max(work_floats, (size_t)pl->team_grid * pl->team_slab);
   }
-  {
-    size_t off = 2 * cmpc::kNumBins;
-    for (int k = 0; k < kNumGroups; ++k) {
-      pl->race_off[k] = off;
-      off += pl->grid[k];
-    }
-    pl->race_state = off;
-  }
-  if (const char* r = getenv("CMPC_RACE")) pl->race = atoi(r) != 0;  // A/B switch
-  e = hipMalloc(&pl->d_counters, (pl->race_state + p->max_batch) * sizeof(int));
+  e = hipMalloc(&pl->d_counters, 2 * cmpc::kNumBins * sizeof(int));
   if (e != hipSuccess) { delete pl; return fail(CMPC_E_NOMEM, "hipMalloc counters failed"); }
   e = hipMalloc(&pl->d_work, work_floats * sizeof(float));
   if (e != hipSuccess) {
@@ -244,18 +232,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
-  // the NC >= 160 class's stream gets the device's highest priority: when both solve kernels
-  // are ready, its one-wave-per-SIMD workgroups are placed first, and its slow instances start
-  // at the beginning of the batch instead of after the NC <= 128 class's queue drains
-  int prio_least = 0, prio_greatest = 0;
-  if ((e = hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest)) != hipSuccess) {
-    cmpc_plan_destroy(pl);
-    return hip_fail(e, "hipDeviceGetStreamPriorityRange");
-  }
-  int prio = prio_greatest;
-  if (const char* sp = getenv("CMPC_SIDE_PRIO"))  // A/B switch: 0 = default priority
-    if (atoi(sp) == 0) prio = 0;
-  if ((e = hipStreamCreateWithPriority(&pl->side, hipStreamNonBlocking, prio)) != hipSuccess ||
+  if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->join, hipEventDisableTiming)) != hipSuccess) {
     cmpc_plan_destroy(pl);
@@ -332,17 +309,11 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  cmpc::Race race{nullptr, nullptr, 0, pl->d_counters, pl->d_counters + cmpc::kNumBins};
-  if (pl->race) {
-    race.state = pl->d_counters + pl->race_state;
-    race.inflight = pl->d_counters + pl->race_off[k];
-    race.slots = (int)g;
-  }
   hipLaunchKernelGGL(group_fn(k, ipm), dim3(g), dim3(64), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
-                     pl->slab[k], race);
+                     pl->slab[k]);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "solve_group_kernel launch");
   if (rec_this) {
@@ -397,22 +368,14 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
   // tail-bound batch: the kernel variants with the interior-point fallback
   const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
-  const bool team = B <= team_batch(pl);
-  // the racing state (zero inflight tables and per-instance states) lies right after the
-  // counters: one memset clears both
-  const size_t race_ints = (team || !pl->race) ? 0 : pl->race_state - 2 * cmpc::kNumBins + B;
   if (B <= 1024) {  // one workgroup bins the batch and zeroes the queue heads (no memset)
-    if (race_ints > 0) {
-      e = hipMemsetAsync(pl->d_counters + 2 * cmpc::kNumBins, 0, race_ints * sizeof(int), st);
-      if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
-    }
     hipLaunchKernelGGL(cmpc::bin_small_kernel, dim3(1), dim3(1024), 0, st, pl->kp.N, (int)B,
                        in.contact, pl->d_counters, pl->d_counters + cmpc::kNumBins, pl->d_lists,
                        pl->p.max_batch);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "bin_small_kernel launch");
   } else {
-    e = hipMemsetAsync(pl->d_counters, 0, (2 * cmpc::kNumBins + race_ints) * sizeof(int), st);
+    e = hipMemsetAsync(pl->d_counters, 0, 2 * cmpc::kNumBins * sizeof(int), st);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
     const int threads = 256;
     const unsigned blocks = (unsigned)((B + threads - 1) / threads);
@@ -424,7 +387,7 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // small batches: a team of kTeamWaves waves per QP, all bins in one kernel on the caller's
   // stream (measured faster than one wave per QP up to B = 4 x CUs on configs 1-3, slower from
   // 2,048 up: DESIGN.md 4g)
-  if (team) return record_team_launch(pl, st, kp, in, out, B);
+  if (B <= team_batch(pl)) return record_team_launch(pl, st, kp, in, out, B);
   // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
   // fills them); it exists only when a step can hold more than 128 / 12 stance legs
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;

@@ -1301,75 +1301,6 @@ __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M
 #include "cmpc_team.hip"  // W waves per QP for small batches (leader + helpers)
 
 // ------------------------------------------------------------------------------------------
-// Racing the stragglers.  A batch ends with its slowest instances: a few per thousand whose
-// active-set repairs cycle take 10-30x the mean, and they may start last.  Once every queue of the
-// solve is drained, a wave that would exit instead restarts one of its kernel's instances still in
-// flight with a different rho0 (kRaceScale: the ADMM trajectory -- and with it the face sets the
-// polish sessions start from -- changes; NumPy model: the best of {4, 16, 1/4, 64} x rho0 needs
-// 2-6x fewer factorizations than the unlucky original on most slow instances).  Up to kMaxRacers
-// racers per instance; the first to finish claims the instance (one atomic) and writes its
-// outputs, the others -- the original included -- notice at their next polish session or 16th
-// ADMM iteration and drop their work.  Any racer's answer is a KKT-verified optimum of the same
-// QP, so which one wins does not change the result beyond the solver tolerance.
-// A wave with nothing to race exits: no wave ever waits for another.
-// ------------------------------------------------------------------------------------------
-constexpr int kRaceDone = 1 << 29;    // Race::state bit: the instance's outputs are claimed
-constexpr int kRaceSecond = 1 << 30;  // Race::inflight bit: the instance is in the kernel's 2nd bin
-constexpr int kMaxRacers = 4;
-__device__ constexpr float kRaceScale[kMaxRacers] = {4.f, 16.f, 0.25f, 64.f};
-
-struct Race {
-  int* state;         // per instance: kRaceDone once claimed, low byte = racers started (null: off)
-  int* inflight;      // per wave slot of this kernel: instance + 1 (| kRaceSecond), 0 = none
-  int slots;
-  const int* counts;  // every bin's count ...
-  const int* heads;   // ... and queue head: racing starts once all queues are drained
-};
-
-__device__ __forceinline__ int race_load(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Has another racer already claimed instance b?
-__device__ __forceinline__ bool race_lost(const Race* rc, int64_t b) {
-  if (rc == nullptr) return false;
-  return (uniform(race_load(rc->state + b)) & kRaceDone) != 0;
-}
-
-// A straggler to race: an in-flight instance of this kernel with fewer than kMaxRacers racers,
-// once every queue of the solve is drained.  False: nothing to do (the wave exits).
-__device__ __forceinline__ bool race_pick(const Race& rc, int64_t& b, bool& second, int& racer) {
-  const int lane = opaque_lane();
-  int pend = 0;
-  if (lane < kNumBins) pend = race_load(rc.heads + lane) < rc.counts[lane];
-  if (__any(pend)) return false;
-  const int start = (int)((blockIdx.x * 97u) % (unsigned)rc.slots);
-  for (int s0 = 0; s0 < rc.slots; s0 += 64) {
-    const int k = s0 + lane;
-    int v = 0, st = kRaceDone;
-    if (k < rc.slots) v = race_load(rc.inflight + (start + k) % rc.slots);
-    if (v != 0) st = race_load(rc.state + ((v & (kRaceSecond - 1)) - 1));
-    unsigned long long m = __ballot(v != 0 && !(st & kRaceDone) && (st & 0xff) < kMaxRacers);
-    while (m) {
-      const int f = __ffsll((long long)m) - 1;
-      const int vf = __builtin_amdgcn_readlane(v, f);
-      const int bf = (vf & (kRaceSecond - 1)) - 1;
-      int old = 0;
-      if (lane == 0) old = atomicAdd(rc.state + bf, 1);
-      old = uniform(old);
-      if (!(old & kRaceDone) && (old & 0xff) < kMaxRacers) {
-        b = bf;
-        second = (vf & kRaceSecond) != 0;
-        racer = old & 0xff;
-        return true;
-      }
-      m &= m - 1;
-    }
-  }
-  return false;
-}
-
-// ------------------------------------------------------------------------------------------
 // Interior-point identification of the face set, for hard instances.  A few instances per
 // thousand keep ADMM's face set "stable" but wrong for a long time: their polish sessions fail,
 // repair, fail again, and the instance runs 100-200 ADMM iterations and 20-45 factorizations
@@ -1494,8 +1425,7 @@ __device__ __forceinline__ void ipm_sync() {
 template <int NC>
 __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
                                              f4 (&M)[Cfg<NC>::NTL], float* __restrict__ park,
-                                             int n, int ntri, const Race* rc, int64_t b,
-                                             bool tr = false) {
+                                             int n, int ntri, bool tr = false) {
   static_assert(offsetof(Smem<NC>, v) == offsetof(Smem<NC>, y) + NC * sizeof(float),
                 "y and v are one free 2 NC block during the interior-point steps");
   const float mu = P.mu, fzm = P.fz_min;
@@ -1529,7 +1459,6 @@ __device__ __forceinline__ bool ipm_identify(Smem<NC>& s, const KParams& P,
   const float m_inv = 1.f / (5.f * (float)max(ntri, 1));
   float mu_first = 0.f;
   for (int it = 0; it < kIpmIters; ++it) {
-    if (race_lost(rc, b)) return false;  // another racer claimed the instance
     gradient<NC>(s, P, n, s.x, s.g);  // grad f(u)
     float mu_c;
     {
@@ -1737,13 +1666,11 @@ __device__ __forceinline__ bool tried_before(Smem<NC>& s, int ntri, int ntried) 
 
 // ------------------------------------------------------------------------------------------
 // IPM: this kernel variant carries the interior-point fallback (tail-bound batches)
-// rc: racing (null: off); rho_scale: this run's rho0 multiplier (a racer's kRaceScale)
 template <int NC, int W, bool IPM = false>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
                                                float* __restrict__ park, TeamSmem<NC, W>* ts,
-                                               int* seq, const Race* rc = nullptr,
-                                               float rho_scale = 1.f) {
+                                               int* seq) {
   // W = 1: the whole lower triangle in this wave's registers; W > 1: this wave's team slots
   f4 M[TeamCfg<NC, W>::SLOTS];
   static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
@@ -1811,8 +1738,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   // in fewer iterations from rho0 / 2; its hard instances (a failed polish session) go back to
   // rho0, where they converge as before (cfg1 +6-10 %, cfg2 +1 %; rho0 / 2 for every bin loses
   // 7 % on cfg2)
-  const float rho0 = uniformf(P.rho0 * rho_scale);
-  float rho = (NC == 128) ? 0.5f * rho0 : rho0;
+  float rho = (NC == 128) ? 0.5f * P.rho0 : P.rho0;
   bool rho_low = NC == 128;  // still at the bin's reduced initial rho
   s.pcode[lane] = -1;
   if (in.w_init == nullptr && in.y_init == nullptr && in.lam_init == nullptr) {
@@ -1915,12 +1841,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     shift = P.sigma;
     in_polish = true;
   }
-  bool lost = false;  // another racer claimed this instance: drop the work
   while (n > 0) {
-    if ((in_polish || (it & 15) == 0) && race_lost(rc, b)) {
-      lost = true;
-      break;
-    }
     if (refactor) {  // the only condense + invert call site
       CMPC_CNT(8, 1);
       ++nfact;
@@ -2029,7 +1950,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         // nothing is parked before the second session, so it would refactor anyway)
         fail_rho_done = true;
         rho_low = false;
-        rho = uniformf(kFailRho * rho0);
+        rho = uniformf(kFailRho * P.rho0);
         shift = uniformf(P.sigma + rho);
         refactor = true;
         continue;
@@ -2045,9 +1966,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           float* keep = park + Cfg<NC>::NTL * 256;
           ipm_save<NC>(s, keep, n);
 #ifdef CMPC_TRACE
-          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri, rc, b, b == CMPC_TRACE);
+          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri, b == CMPC_TRACE);
 #else
-          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri, rc, b);
+          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri);
 #endif
           parked = false;
           if (!ok_ipm) {  // (non-finite steps) back to ADMM as it was, refactoring first
@@ -2071,7 +1992,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       }
       if (rho_low) {  // a hard instance: back to the standard rho0 (one refactor)
         rho_low = false;
-        rho = rho0;
+        rho = uniformf(P.rho0);
         shift = uniformf(P.sigma + rho);
         refactor = true;
         continue;
@@ -2212,18 +2133,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       in_polish = true;
     }
   }
-  if (lost) return;
   if (!polished) {
     if (n > 0) {
       const bool conv = rp <= P.eps_abs + P.eps_rel * np_ && rd <= P.eps_abs + P.eps_rel * nd;
       status = conv ? 2 : -2;
     }
     gradient<NC, (W > 1)>(s, P, n, s.z, s.g, pwc, twc);  // E at u = z (the pure rollout when every leg swings)
-  }
-  if (rc != nullptr) {  // claim the instance: the first racer to finish writes its outputs
-    int won = 0;
-    if (lane == 0) won = (atomicOr(rc->state + b, kRaceDone) & kRaceDone) == 0;
-    if (uniform(won) == 0) return;
   }
   CMPC_T0(t_out);
   // ---- outputs: x_{k+1} = e_{k+1} + xref_k, u from the triples (zero on swing legs) ----
@@ -2313,8 +2228,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     out.iters[b] = iters + 1000 * dg_pol + 1000000 * dg_fact;
 #elif defined(CMPC_DIAG_TIMES)  // start (10 ns ticks, low 31 bits) | duration + 1e9 if teamed
     out.status[b] = (int)(dt_t0 & 0x7fffffffull);
-    out.iters[b] = (int)(__builtin_amdgcn_s_memrealtime() - dt_t0) +
-                   (rho_scale != 1.f ? 1000000000 : 0);  // a racer won
+    out.iters[b] = (int)(__builtin_amdgcn_s_memrealtime() - dt_t0) ;
 #else
     out.status[b] = status;
     out.iters[b] = iters;
@@ -2352,70 +2266,33 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
 
 // One persistent kernel per register class: bins NCA and NCB share the occupancy (two waves per
 // SIMD for NC <= 128, one for NC >= 160), so one kernel serves both, draining the larger bin
-// first (its instances are the slower ones: hardest first shortens the batch tail), then racing
-// the class's stragglers (Race).  Two kernels instead of four keep the solve within the device's
-// hardware queues (the caller's stream + one plan stream).  IPM: the variant with the
+// first (its instances are the slower ones: hardest first shortens the batch tail).  Two
+// kernels instead of four keep the solve within the device's hardware queues (the caller's
+// stream + one plan stream), so the two classes really overlap.  IPM: the variant with the
 // interior-point fallback for hard instances (used for tail-bound batches).
 template <int NCA, int NCB, bool IPM>
 __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
     solve_group_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
                        const int* __restrict__ list_b, const int* __restrict__ counts,
                        int* __restrict__ heads, int qa, float* __restrict__ work,
-                       size_t slab, Race rc) {
+                       size_t slab) {
   static_assert(Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
   constexpr size_t kBytes = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
                                                                    : sizeof(Smem<NCB>);
   __shared__ __attribute__((aligned(16))) unsigned char raw[kBytes];
   float* park = work + (size_t)blockIdx.x * slab;
-  Smem<NCA>& sa = *reinterpret_cast<Smem<NCA>*>(raw);
-  Smem<NCB>& sb = *reinterpret_cast<Smem<NCB>*>(raw);
-  const int lane = opaque_lane();
 #ifdef CMPC_STAMPS
   // st[] is the first member of every Smem<NC>: one set of totals for the wave
-  if (threadIdx.x < 32) sa.st[threadIdx.x] = 0;
+  Smem<NCA>& s0 = *reinterpret_cast<Smem<NCA>*>(raw);
+  if (threadIdx.x < 32) s0.st[threadIdx.x] = 0;
 #endif
-  const Race* rcp = (rc.state != nullptr) ? &rc : nullptr;
-  const int total_a = counts[qa], total_b = counts[qa - 1];
-  int phase = 0;  // 0: the larger bin's queue, 1: the smaller bin's, 2: racing
-  for (;;) {
-    int64_t b = 0;
-    bool second = false;
-    int racer = -1;
-    if (phase < 2) {
-      int idx = 0;
-      if (lane == 0) idx = atomicAdd(heads + (phase == 0 ? qa : qa - 1), 1);
-      idx = __builtin_amdgcn_readfirstlane(idx);
-      if (idx >= (phase == 0 ? total_a : total_b)) {
-        ++phase;
-        continue;
-      }
-      second = phase == 1;
-      b = (second ? list_b : list_a)[idx];
-    } else if (rcp == nullptr || !race_pick(rc, b, second, racer)) {
-      break;
-    }
-    if (rcp != nullptr && racer < 0 && lane == 0)
-      rc.inflight[blockIdx.x] = (int)(b + 1) | (second ? kRaceSecond : 0);
-    const float scale = (racer < 0) ? 1.f : kRaceScale[racer];
-    WSYNC();
-    if (second) {
-      if (lane < 12) {  // KParams copies (each bin's Smem layout places them differently)
-        sb.Q2[lane] = P.Q2[lane];
-        sb.R2[lane] = P.R2[lane];
-      }
-      solve_instance<NCB, 1, IPM>(sb, P, b, in, out, park, nullptr, nullptr, rcp, scale);
-    } else {
-      if (lane < 12) {
-        sa.Q2[lane] = P.Q2[lane];
-        sa.R2[lane] = P.R2[lane];
-      }
-      solve_instance<NCA, 1, IPM>(sa, P, b, in, out, park, nullptr, nullptr, rcp, scale);
-    }
-    if (rcp != nullptr && racer < 0 && lane == 0) rc.inflight[blockIdx.x] = 0;
-  }
+  drain_bin<NCA, 1, IPM>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa,
+                         heads + qa, park);
+  drain_bin<NCB, 1, IPM>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
+                         heads + qa - 1, park);
 #ifdef CMPC_STAMPS
   WSYNC();
-  if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], sa.st[threadIdx.x]);
+  if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
 #endif
 }
 
