@@ -773,33 +773,39 @@ def aux_objects(args, plan, full, dev, stream, torch):
         loop = {"plant": "cmpc_srb_step single-rigid-body stand-in (MuJoCo absent)",
                 "mpc_dt_s": 1 / 48}
         for nb in (1024, B):
-            cl = ClosedLoop(nb, plan=plan, seed=0)
+            # eager and graph replay on the same tick sequence: two loops from the same seed,
+            # 5 untimed ticks each (the graph's capture records tick 5, its first replay runs
+            # it), then ticks 6 .. 5 + loop_steps timed
             rg = np.random.default_rng(100)
-            cl.set_command(np.stack([rg.uniform(-0.5, 0.5, nb), rg.uniform(-0.2, 0.2, nb),
-                                     np.full(nb, 0.27), rg.uniform(-1, 1, nb)], 1))
-            for _ in range(4):
+            cmd = np.stack([rg.uniform(-0.5, 0.5, nb), rg.uniform(-0.2, 0.2, nb),
+                            np.full(nb, 0.27), rg.uniform(-1, 1, nb)], 1)
+            rate = {}
+            for mode in ("eager", "graph"):
+                cl = ClosedLoop(nb, plan=plan, seed=0)
+                cl.set_command(cmd)
+                for _ in range(4):
+                    cl.tick()
+                if mode == "graph":
+                    cl.capture()
                 cl.tick()
-            sync()
-            te = time.perf_counter()
-            for _ in range(args.loop_steps):
-                cl.tick()
-            sync()
-            eager = nb * args.loop_steps / (time.perf_counter() - te)
-            cl.capture()
-            cl.tick()
-            sync()
-            tg = time.perf_counter()
-            for _ in range(args.loop_steps):
-                cl.tick()
-            sync()
-            el = time.perf_counter() - tg
-            loop[f"robots_{nb}"] = {"robot_ticks_per_s_graph": nb * args.loop_steps / el,
-                                    "ms_per_tick_graph": el / args.loop_steps * 1e3,
-                                    "robot_ticks_per_s_eager": eager,
-                                    "solved_frac": float((cl.status == 1).float().mean().item()),
-                                    "iters_mean": float(cl.iters.float().mean().item()),
-                                    "com_z_min": float(cl.x[:, 2].min().item())}
-            del cl
+                sync()
+                t0 = time.perf_counter()
+                for _ in range(args.loop_steps):
+                    cl.tick()
+                sync()
+                el = time.perf_counter() - t0
+                rate[mode] = (nb * args.loop_steps / el, el / args.loop_steps * 1e3)
+                if mode == "graph":
+                    loop[f"robots_{nb}"] = {
+                        "robot_ticks_per_s_graph": rate["graph"][0],
+                        "ms_per_tick_graph": rate["graph"][1],
+                        "robot_ticks_per_s_eager": rate["eager"][0],
+                        "ms_per_tick_eager": rate["eager"][1],
+                        "ticks": f"6..{5 + args.loop_steps} in both modes",
+                        "solved_frac": float((cl.status == 1).float().mean().item()),
+                        "iters_mean": float(cl.iters.float().mean().item()),
+                        "com_z_min": float(cl.x[:, 2].min().item())}
+                del cl
         out["closed_loop"] = loop
 
     # BASELINE config 0: one robot through the reference's own API (CentroidalMPC.solve_QP, the

@@ -97,7 +97,10 @@ class ClosedLoop:
         # what generate_traj reads off the robot: levers COM -> foot, I_com in the world frame
         torch.sub(self.feet, self.x[:, None, 0:3], out=self.lever)
         R = rot_zyx(self.x[:, 3:6])
-        torch.matmul(torch.matmul(R, self.I_body), R.transpose(1, 2), out=self.I_world)
+        # R I_body R' as broadcast products + size-3 sums: batched 3x3 GEMMs go to the BLAS
+        # library, two launches of ~0.57 ms each at 65,536 robots (rocprofv3, tools/loop_graph.py)
+        RI = (R[:, :, :, None] * self.I_body[:, None, :, :]).sum(2)
+        torch.sum(RI[:, :, None, :] * R[:, None, :, :], 3, out=self.I_world)
         p.generate_traj(self.x, self.pos_des, self.cmd, self.t, self.gait, self.lever, self.hip,
                         self.dt, out=(self.xref, self.ct, self.rf), stream=stream)
         p.build_dynamics(self.mass, self.I_world, self.rf, self.xref, self.dt,

@@ -388,23 +388,30 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // stream (measured faster than one wave per QP up to B = 4 x CUs on configs 1-3, slower from
   // 2,048 up: DESIGN.md 4g)
   if (B <= team_batch(pl)) return record_team_launch(pl, st, kp, in, out, B);
-  // the one-wave-per-SIMD class first (its waves take whole SIMDs before the two-wave class
-  // fills them); it exists only when a step can hold more than 128 / 12 stance legs
+  // The two classes run concurrently: the NC <= 128 class on the caller's stream, the NC >= 160
+  // class (it exists only when a step can hold more than 128 / 12 stance legs) on the plan
+  // stream, forked after the binning and joined back.  The NC <= 128 class is submitted first:
+  // its two waves per SIMD fill the device and the NC >= 160 waves (one per SIMD) take SIMDs as
+  // they free up.  Placed the other way round -- what a HIP graph did when the heavy launch
+  // came first in capture order -- the NC <= 128 kernel ran with ~1,570 of its 2,048 waves
+  // resident and 20-25 % slower (tools/diag_times.py, tools/loop_graph.py).
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
-    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, pl->side, kp, in, out, g1, ipm);
-    if (rc != CMPC_OK) return rc;
-    if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
   rc = record_launch(pl, 0, st, kp, in, out, g0, ipm);
   if (rc != CMPC_OK) return rc;
-  if (big && (e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
-    return hip_fail(e, "hipStreamWaitEvent");
+  if (big) {
+    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+    rc = record_launch(pl, 1, pl->side, kp, in, out, g1, ipm);
+    if (rc != CMPC_OK) return rc;
+    if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
+      return hip_fail(e, "hipStreamWaitEvent");
+  }
   return CMPC_OK;
 }
 

@@ -30,8 +30,8 @@ def main():
         for _ in range(4):
             cl.tick()
         if mode.startswith("graph"):
-            cl.capture()
-            cl.tick()
+            cl.capture()  # records tick 5 without running it
+        cl.tick()  # tick 5 (the graph's first replay): both modes then time ticks 6 .. 5 + T
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(T):
