@@ -1666,11 +1666,32 @@ __device__ __forceinline__ bool tried_before(Smem<NC>& s, int ntri, int ntried) 
 
 // ------------------------------------------------------------------------------------------
 // IPM: this kernel variant carries the interior-point fallback (tail-bound batches)
+// The interior-point stage runs outside solve_instance (drain_bin calls it between two calls of
+// solve_instance): inlined inside the solve loop it shared that loop's register allocation and
+// spilled on the hot path.  Resume carries the loop state across it.
+struct Resume {
+  int stage;  // 0: a new instance; 1: the interior-point stage is due; 2: resume after it
+  bool ipm_ok, rho_low, seen_start, fail_rho_done;
+  float rho, rp, rd, np_, nd;
+  int n, ntri, status, iters, it, nfail, ntried, last_pol, nsfail, nfact;
+#ifdef CMPC_DIAG_COUNTS
+  int dg_fact, dg_pol;
+  unsigned long long dg_t0;
+#endif
+#ifdef CMPC_DIAG_TIMES
+  unsigned long long dt_t0;
+#endif
+};
+
 template <int NC, int W, bool IPM = false>
 __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, int64_t b,
                                                const Inputs& in, const Outputs& out,
                                                float* __restrict__ park, TeamSmem<NC, W>* ts,
-                                               int* seq) {
+                                               int* seq, Resume* rs = nullptr) {
+  // resuming after the interior-point stage: LDS still holds the instance (inputs, basis,
+  // ADMM state parked by ipm_save), the loop state comes from rs
+  bool resume = false;
+  if constexpr (W == 1 && IPM) resume = rs->stage == 2;
   // W = 1: the whole lower triangle in this wave's registers; W > 1: this wave's team slots
   f4 M[TeamCfg<NC, W>::SLOTS];
   static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
@@ -1687,7 +1708,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   CMPC_CNT(10, 1);
 
   WSYNC();
-  {  // one round of global loads: A, r_0..r_N (= x0, xref), gd; staged in LDS (G is free here)
+  if (!resume) {  // one round of global loads: A, r_0..r_N (= x0, xref), gd; staged in LDS (G is free here)
     float av[3], rv[4];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -1716,15 +1737,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   if (stc) s.tri[pos] = lane;
   if (lane < 4 * N) s.tri_of[lane] = stc ? pos : -1;
   WSYNC();
-  for (int o = lane; o < NP; o += 64) {  // d_k = A r_k + gd - r_{k+1}, r_0 = x0
-    const int k = o / 12, r = o % 12;
-    const float* rk = &s.G[12 * k];
-    float acc = s.G[256 + r] - rk[12 + r];
+  if (!resume) {
+    for (int o = lane; o < NP; o += 64) {  // d_k = A r_k + gd - r_{k+1}, r_0 = x0
+      const int k = o / 12, r = o % 12;
+      const float* rk = &s.G[12 * k];
+      float acc = s.G[256 + r] - rk[12 + r];
 #pragma unroll
-    for (int j = 0; j < 12; ++j) acc = fmaf(s.A[r * 12 + j], rk[j], acc);
-    s.D[o] = acc;
+      for (int j = 0; j < 12; ++j) acc = fmaf(s.A[r * 12 + j], rk[j], acc);
+      s.D[o] = acc;
+    }
+    build_admm_basis<NC>(s, P, Bg, ntri);
   }
-  build_admm_basis<NC>(s, P, Bg, ntri);
   const int n = 3 * ntri;
   // team mode: the gradient's powers of A once per instance (registers to spare: the tiles are
   // split over the team)
@@ -1740,8 +1763,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   // 7 % on cfg2)
   float rho = (NC == 128) ? 0.5f * P.rho0 : P.rho0;
   bool rho_low = NC == 128;  // still at the bin's reduced initial rho
-  s.pcode[lane] = -1;
-  if (in.w_init == nullptr && in.y_init == nullptr && in.lam_init == nullptr) {
+  if (!resume) s.pcode[lane] = -1;
+  if (resume) {
+  } else if (in.w_init == nullptr && in.y_init == nullptr && in.lam_init == nullptr) {
     for (int p = lane; p < n; p += 64) { s.x[p] = 0.f; s.z[p] = 0.f; s.y[p] = 0.f; }
   } else if (lane < ntri) {
     // warm start (the reference's x0 / lam_x0 of centroidal_mpc.py:91-95): triple `lane`
@@ -1804,10 +1828,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int status = -2, iters = 0;
 #ifdef CMPC_DIAG_COUNTS
   int dg_fact = 0, dg_pol = 0;
-  const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
+  unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef CMPC_DIAG_TIMES  // diagnostic build: start / end on the 100 MHz constant clock
-  const unsigned long long dt_t0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long dt_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   bool polished = false;
   float rp = 0.f, rd = 0.f, np_ = 0.f, nd = 0.f;
@@ -1830,7 +1854,37 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   bool fail_rho_done = false;  // rho moved to kFailRho x rho0 after the first failed session
   const float alpha = P.alpha;
   if (n == 0) status = 1;
-  if (n > 0 && in.w_init != nullptr) {
+  if constexpr (W == 1 && IPM) {
+    if (resume) {
+      rho = rs->rho; rho_low = rs->rho_low; rp = rs->rp; rd = rs->rd; np_ = rs->np_; nd = rs->nd;
+      status = rs->status; iters = rs->iters; it = rs->it; nfail = rs->nfail; ntried = rs->ntried;
+      last_pol = rs->last_pol; nsfail = rs->nsfail; nfact = rs->nfact;
+      seen_start = rs->seen_start; fail_rho_done = rs->fail_rho_done;
+#ifdef CMPC_DIAG_COUNTS
+      dg_fact = rs->dg_fact; dg_pol = rs->dg_pol; dg_t0 = rs->dg_t0;
+#endif
+#ifdef CMPC_DIAG_TIMES
+      dt_t0 = rs->dt_t0;
+#endif
+      ipm_done = true;
+      parked = false;
+      if (!rs->ipm_ok) {  // (non-finite steps) back to ADMM as it was, refactoring first
+        ipm_restore<NC>(s, park + Cfg<NC>::NTL * 256, n);
+        shift = uniformf(P.sigma + rho);
+      } else {  // polish the interior point's face set with the full repair budget
+        ipm_session = true;
+        session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
+        seen_start = false;
+        repairs_left = P.polish_repairs;
+        nact = polish_setup<NC>(s, P, Bg, ntri);
+        shift = P.sigma;
+        in_polish = true;
+        last_pol = it;
+        stable = -(P.polish_stable << min(nfail, kBackoffCap));
+      }
+    }
+  }
+  if (!resume && n > 0 && in.w_init != nullptr) {
     // warm active set: the face set of the warm point goes straight to the polish (one
     // reduced factorization instead of the ADMM one + the polish one); if its KKT check and
     // repairs fail, ADMM starts from the warm (x, z, y) as above
@@ -1963,31 +2017,21 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #ifdef CMPC_DIAG_COUNTS
           dg_pol += 100;  // (diagnostic: the interior-point fallback ran)
 #endif
-          float* keep = park + Cfg<NC>::NTL * 256;
-          ipm_save<NC>(s, keep, n);
-#ifdef CMPC_TRACE
-          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri, b == CMPC_TRACE);
-#else
-          const bool ok_ipm = ipm_identify<NC>(s, P, M, park, n, ntri);
+          ipm_save<NC>(s, park + Cfg<NC>::NTL * 256, n);
+          // the stage runs in drain_bin, which then calls solve_instance again to resume here
+          rs->stage = 1;
+          rs->n = n; rs->ntri = ntri;
+          rs->rho = rho; rs->rho_low = rho_low; rs->rp = rp; rs->rd = rd; rs->np_ = np_; rs->nd = nd;
+          rs->status = status; rs->iters = iters; rs->it = it; rs->nfail = nfail;
+          rs->ntried = ntried; rs->last_pol = last_pol; rs->nsfail = nsfail; rs->nfact = nfact;
+          rs->seen_start = seen_start; rs->fail_rho_done = fail_rho_done;
+#ifdef CMPC_DIAG_COUNTS
+          rs->dg_fact = dg_fact; rs->dg_pol = dg_pol; rs->dg_t0 = dg_t0;
 #endif
-          parked = false;
-          if (!ok_ipm) {  // (non-finite steps) back to ADMM as it was, refactoring first
-            ipm_restore<NC>(s, keep, n);
-            refactor = true;
-            shift = uniformf(P.sigma + rho);
-            continue;
-          }
-          ipm_session = true;
-          session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
-          seen_start = false;
-          repairs_left = P.polish_repairs;
-          nact = polish_setup<NC>(s, P, Bg, ntri);
-          shift = P.sigma;
-          refactor = true;
-          in_polish = true;
-          last_pol = it;
-          stable = -(P.polish_stable << min(nfail, kBackoffCap));
-          continue;
+#ifdef CMPC_DIAG_TIMES
+          rs->dt_t0 = dt_t0;
+#endif
+          return;
         }
       }
       if (rho_low) {  // a hard instance: back to the standard rho0 (one refactor)
@@ -2259,7 +2303,24 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
     if (lane == 0) idx = atomicAdd(head, 1);
     idx = __builtin_amdgcn_readfirstlane(idx);
     if (idx >= total) break;
-    solve_instance<NC, W, IPM>(s, P, (int64_t)list[idx], in, out, park, ts, seq);
+    const int64_t b = list[idx];
+    if constexpr (W == 1 && IPM) {
+      Resume rs;
+      rs.stage = 0;
+      for (;;) {  // (one call site of each: the stage runs with none of the solve's state live)
+        solve_instance<NC, W, IPM>(s, P, b, in, out, park, ts, seq, &rs);
+        if (rs.stage != 1) break;
+        f4 M[Cfg<NC>::NTL];
+#ifdef CMPC_TRACE
+        rs.ipm_ok = ipm_identify<NC>(s, P, M, park, rs.n, rs.ntri, b == CMPC_TRACE);
+#else
+        rs.ipm_ok = ipm_identify<NC>(s, P, M, park, rs.n, rs.ntri);
+#endif
+        rs.stage = 2;
+      }
+    } else {
+      solve_instance<NC, W, IPM>(s, P, b, in, out, park, ts, seq);
+    }
   }
   if constexpr (W > 1) team_issue<NC, W>(*ts, *seq, kOpExit, 0, 0, 0);
 }
