@@ -103,7 +103,7 @@ def parse(argv=None):
     ap.add_argument("--traffic-json", type=str, default=str(REPO / "profiles" / "hbm_traffic.json"),
                     help="PMC-derived HBM bytes per launch of the dominant kernel (profiles/)")
     ap.add_argument("--counters-json", type=str,
-                    default=str(REPO / "profiles" / "r02_counters.json"),
+                    default=str(REPO / "profiles" / "counters.json"),
                     help="PMC instruction counters of the dominant kernel (profiles/)")
     ap.add_argument("--sub-configs", type=int, default=1,
                     help="N = 1: also time configs 1 / 2 at their own and at 65,536 (0 = skip)")

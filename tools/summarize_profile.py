@@ -6,7 +6,7 @@ Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats of the headline run),
 profiles/<tag>_kernel_trace_solve.csv (the solve-kernel rows of its trace: queue, start, end),
 profiles/<tag>_hbm_traffic.json + profiles/hbm_traffic.json (PMC HBM bytes per launch of the
 dominant kernel, the bench's ``roofline.traffic``), profiles/<tag>_counters.json +
-profiles/r02_counters.json (instruction-mix counters per launch: MFMA count, matrix-pipe
+profiles/counters.json (instruction-mix counters per launch: MFMA count, matrix-pipe
 busy fraction, FP32 matrix TFLOP/s from the counted MFMAs), and copies the bench line.
 
 Counter conventions (/opt/skills/guides/MI355X_MICROARCH.md): FETCH_SIZE / WRITE_SIZE in KB,
@@ -47,7 +47,7 @@ def main():
     ap.add_argument("--root", default=str(REPO / "gpurun_out"))
     ap.add_argument("--side", action="store_true",
                     help="a side profile (not the headline): leave profiles/hbm_traffic.json and "
-                         "r02_counters.json alone")
+                         "profiles/counters.json alone")
     a = ap.parse_args()
     root = Path(a.root)
     out = REPO / "profiles"
@@ -101,8 +101,8 @@ def main():
                 s["mfma_frac_of_peak"] = s["mfma_tflops_at_trace_ms"] / PEAK_TFS
         summary[name] = s
     (out / f"{a.tag}_counters.json").write_text(json.dumps(summary, indent=1))
-    if a.tag != "r02" and not a.side:
-        (out / "r02_counters.json").write_text(json.dumps(summary, indent=1))
+    if not a.side:  # the bench's default --counters-json (the latest headline profile)
+        (out / "counters.json").write_text(json.dumps(summary, indent=1))
     # dominant kernel (longest median trace duration) -> the bench's traffic figure
     dom = max(summary, key=lambda n: summary[n].get("trace_ms_median", 0.0)) if summary else None
     if dom and "hbm_bytes_per_launch" in summary[dom]:
