@@ -43,8 +43,8 @@ class CParams(ctypes.Structure):
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
            "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_plan_set_team", "cmpc_plan_team_batch",
-           "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch", "cmpc_plan_solve_kernel",
-           "cmpc_last_error",
+           "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch", "cmpc_plan_set_heavy_first",
+           "cmpc_plan_heavy_first_batch", "cmpc_plan_solve_kernel", "cmpc_last_error",
            "cmpc_version")
 NUM_BINS = 4
 BIN_CAPS = (96, 128, 160, 192)
@@ -109,6 +109,11 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
         lib.cmpc_plan_set_ipm.restype = ctypes.c_int
         lib.cmpc_plan_ipm_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         lib.cmpc_plan_ipm_batch.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_plan_set_heavy_first"):
+        lib.cmpc_plan_set_heavy_first.argtypes = [vp, ctypes.c_int64]
+        lib.cmpc_plan_set_heavy_first.restype = ctypes.c_int
+        lib.cmpc_plan_heavy_first_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
+        lib.cmpc_plan_heavy_first_batch.restype = ctypes.c_int
     if hasattr(lib, "cmpc_plan_solve_kernel"):
         lib.cmpc_plan_solve_kernel.argtypes = [vp, ctypes.c_int64, ctypes.c_int]
         lib.cmpc_plan_solve_kernel.restype = ctypes.c_char_p

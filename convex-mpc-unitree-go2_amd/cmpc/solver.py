@@ -147,6 +147,20 @@ class Plan:
                "cmpc_plan_ipm_batch")
         return int(v.value)
 
+    def set_heavy_first(self, min_batch: int):
+        """Submit the NC >= 160 register class first for solves of B >= min_batch: -1 =
+        automatic (B > 16 x CUs, the default), 0 = never (cmpc_plan_set_heavy_first)."""
+        _check(self.lib, self.lib.cmpc_plan_set_heavy_first(self._h, int(min_batch)),
+               "cmpc_plan_set_heavy_first")
+
+    def heavy_first_batch(self) -> int:
+        """The smallest batch that submits the NC >= 160 class first, 0 = never
+        (cmpc_plan_heavy_first_batch)."""
+        v = ctypes.c_int64()
+        _check(self.lib, self.lib.cmpc_plan_heavy_first_batch(self._h, ctypes.byref(v)),
+               "cmpc_plan_heavy_first_batch")
+        return int(v.value)
+
     def solve_kernels(self, B: int) -> list:
         """Names of the solve kernels a batch of B launches, per timing slot (None: slot not
         launched), as cmpc_plan_solve_kernel reports them."""

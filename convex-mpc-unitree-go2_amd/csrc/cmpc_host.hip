@@ -40,10 +40,12 @@ struct cmpc_plan {
   // tail-bound batches (B <= ipm_max_batch): the one-wave kernel variants with the
   // interior-point fallback for hard instances
   int64_t ipm_max_batch = -1;   // -1: automatic (B <= 64 x CUs)
+  // batches of B >= heavy_first_min_batch submit the NC >= 160 class first
+  int64_t heavy_first_min_batch = -1;  // -1: automatic (B > 16 x CUs), 0: never
   // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
-  // concurrently: the NC <= 128 class on the caller's stream, the NC >= 160 class on one plan
-  // stream forked from / joined to it.  Two streams in total stay within the device's hardware
-  // queues (GPU_MAX_HW_QUEUES = 4), so the classes overlap instead of sharing a queue.
+  // concurrently, one on the caller's stream (submitted first) and one on a plan stream forked
+  // from / joined to it.  Two streams in total stay within the device's hardware queues
+  // (GPU_MAX_HW_QUEUES = 4), so the classes overlap instead of sharing a queue.
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr;
   hipEvent_t join = nullptr;
@@ -323,6 +325,10 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
   return CMPC_OK;
 }
 
+static int64_t heavy_first_batch(const cmpc_plan* pl) {
+  return pl->heavy_first_min_batch >= 0 ? pl->heavy_first_min_batch : 16LL * pl->cus + 1;
+}
+
 static int64_t team_batch(const cmpc_plan* pl) {
   return pl->team_max_batch >= 0 ? pl->team_max_batch : 4LL * pl->cus;
 }
@@ -388,13 +394,18 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // stream (measured faster than one wave per QP up to B = 4 x CUs on configs 1-3, slower from
   // 2,048 up: DESIGN.md 4g)
   if (B <= team_batch(pl)) return record_team_launch(pl, st, kp, in, out, B);
-  // The two classes run concurrently: the NC <= 128 class on the caller's stream, the NC >= 160
-  // class (it exists only when a step can hold more than 128 / 12 stance legs) on the plan
-  // stream, forked after the binning and joined back.  The NC <= 128 class is submitted first:
-  // its two waves per SIMD fill the device and the NC >= 160 waves (one per SIMD) take SIMDs as
-  // they free up.  Placed the other way round -- what a HIP graph did when the heavy launch
-  // came first in capture order -- the NC <= 128 kernel ran with ~1,570 of its 2,048 waves
-  // resident and 20-25 % slower (tools/diag_times.py, tools/loop_graph.py).
+  // The two classes run concurrently: the class submitted first on the caller's stream, the
+  // other (the NC >= 160 class exists only when a step can hold more than 128 / 12 stance legs)
+  // on the plan stream, forked after the binning and joined back.  Whichever is submitted first
+  // fills the device (two NC <= 128 waves or one NC >= 160 wave per SIMD) and the other takes
+  // SIMDs as they free up, so the classes run almost one after the other and the end of the
+  // step is the tail of the class that runs last (tools/shard_anatomy.py timelines).  Large
+  // batches put the NC >= 160 class first: its tail (one wave per SIMD, ~11 instances per wave)
+  // is then filled by NC <= 128 waves, and the NC <= 128 tail (~26 cheaper instances per wave)
+  // ends the step -- config 3 at 65,536 12.2 -> 11.8 ms, at 16,384 5.5 -> 4.2 ms; small ones
+  // (config 2 at 4,096: 2.0 vs 2.4 ms) keep the NC <= 128 class first.  Heavy-first relies on
+  // the LDS slot padding of solve_group_kernel (cmpc_wave.hip kLdsSlot): without it the
+  // NC <= 128 waves that replace the NC >= 160 ones fit ~6 instead of 8 per CU.
   const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -402,11 +413,13 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
       return hip_fail(e, "hipStreamWaitEvent");
   }
   const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-  rc = record_launch(pl, 0, st, kp, in, out, g0, ipm);
+  const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+  const int64_t hmin = heavy_first_batch(pl);
+  const int first = (big && hmin > 0 && B >= hmin) ? 1 : 0;  // class submitted first
+  rc = record_launch(pl, first, st, kp, in, out, first ? g1 : g0, ipm);
   if (rc != CMPC_OK) return rc;
   if (big) {
-    const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
-    rc = record_launch(pl, 1, pl->side, kp, in, out, g1, ipm);
+    rc = record_launch(pl, 1 - first, pl->side, kp, in, out, first ? g0 : g1, ipm);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
@@ -540,6 +553,19 @@ int cmpc_plan_set_ipm(cmpc_plan* pl, int64_t max_batch) {
 int cmpc_plan_ipm_batch(const cmpc_plan* pl, int64_t* max_batch) {
   if (!pl || !max_batch) return fail(CMPC_E_INVALID, "cmpc_plan_ipm_batch: null argument");
   *max_batch = ipm_batch(pl);
+  return CMPC_OK;
+}
+
+int cmpc_plan_set_heavy_first(cmpc_plan* pl, int64_t min_batch) {
+  if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_heavy_first: null plan");
+  if (min_batch < -1) return fail(CMPC_E_INVALID, "cmpc_plan_set_heavy_first: min_batch must be >= -1");
+  pl->heavy_first_min_batch = min_batch;
+  return CMPC_OK;
+}
+
+int cmpc_plan_heavy_first_batch(const cmpc_plan* pl, int64_t* min_batch) {
+  if (!pl || !min_batch) return fail(CMPC_E_INVALID, "cmpc_plan_heavy_first_batch: null argument");
+  *min_batch = heavy_first_batch(pl);
   return CMPC_OK;
 }
 

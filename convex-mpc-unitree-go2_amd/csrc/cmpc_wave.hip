@@ -2325,6 +2325,18 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
   if constexpr (W > 1) team_issue<NC, W>(*ts, *seq, kOpExit, 0, 0, 0);
 }
 
+// LDS slot: each class kernel's allocation is padded to a multiple of kLdsSlot, so that an
+// NC >= 160 wave's block (2 slots, 39,936 B) is exactly two NC <= 128 blocks (1 slot; 19,632 B
+// used) and the 160 KiB of a CU hold 8 of one or 4 of the other (every power-of-two allocation
+// granule up to 4 KiB rounds both alike).  When the NC >= 160 class runs first and its waves
+// exit one by one, the two NC <= 128 waves that take over each freed SIMD then also fit into
+// the LDS it freed: unpadded (27,056 B), the CU's LDS fragmented and the NC <= 128 kernel ran
+// with ~1,550 of its 2,048 waves resident for the rest of the step (tools/shard_anatomy.py).
+#ifndef CMPC_LDS_SLOT
+#define CMPC_LDS_SLOT 19968
+#endif
+constexpr size_t kLdsSlot = CMPC_LDS_SLOT;
+
 // One persistent kernel per register class: bins NCA and NCB share the occupancy (two waves per
 // SIMD for NC <= 128, one for NC >= 160), so one kernel serves both, draining the larger bin
 // first (its instances are the slower ones: hardest first shortens the batch tail).  Two
@@ -2338,8 +2350,10 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
                        int* __restrict__ heads, int qa, float* __restrict__ work,
                        size_t slab) {
   static_assert(Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
-  constexpr size_t kBytes = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
-                                                                   : sizeof(Smem<NCB>);
+  constexpr size_t kImg = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
+                                                                 : sizeof(Smem<NCB>);
+  constexpr size_t kBytes = kLdsSlot ? (kImg + kLdsSlot - 1) / kLdsSlot * kLdsSlot : kImg;
+  static_assert(!kLdsSlot || 4 * kBytes <= 160 * 1024, "one wave per SIMD must fit the CU's LDS");
   __shared__ __attribute__((aligned(16))) unsigned char raw[kBytes];
   float* park = work + (size_t)blockIdx.x * slab;
 #ifdef CMPC_STAMPS

@@ -242,8 +242,11 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
  * most CMPC_NUM_SOLVE_KERNELS persistent solve kernels; cmpc_plan_solve_kernel names solve
  * kernel k (0 or 1) of a batch of B instances, or returns NULL if that slot is not launched:
  *   B <= cmpc_plan_team_batch:  "solve_team_kernel<4>" (k = 0 only);
- *   larger batches:             "solve_pair_kernel<IPM>" (k = 0 only; IPM = true for
- *                               B <= cmpc_plan_ipm_batch), every bin in one launch on `stream`.
+ *   larger batches:             "solve_group_kernel<128, 96, IPM>" (k = 0, the NC <= 128
+ *                               class) and "solve_group_kernel<192, 160, IPM>" (k = 1, the
+ *                               NC >= 160 class; NULL if N is too short to need it); IPM = true
+ *                               for B <= cmpc_plan_ipm_batch.  Slots are per class, whichever
+ *                               of the two is submitted first (cmpc_plan_set_heavy_first).
  * While enabled, cmpc_solve records a hipEvent pair around each solve-kernel launch on the
  * stream it is launched on; cmpc_plan_timing_read waits for the recorded events, returns the
  * summed milliseconds per kernel slot (ms_per_kernel[CMPC_NUM_SOLVE_KERNELS]) and the launch
@@ -271,6 +274,18 @@ int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
  * B <= 64 x CUs; 0 never.  cmpc_plan_ipm_batch returns the effective bound. */
 int cmpc_plan_set_ipm(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_ipm_batch(const cmpc_plan* plan, int64_t* max_batch);
+
+/* Launch order of the two register classes.  A batch above the small-batch bound launches one
+ * persistent kernel per register class (NC <= 128: two waves per SIMD; NC >= 160: one); the
+ * class submitted first fills the device and the other takes SIMDs as they free up, so the
+ * step ends with the tail of the class that runs second.  Batches of B >= min_batch submit the
+ * NC >= 160 class first (its tail is then filled by NC <= 128 waves: config 3 at 65,536 and
+ * 16,384 faster), smaller ones the NC <= 128 class (config 2 at 4,096 faster).  Results do not
+ * depend on the order (each instance is solved by one wave, deterministically).
+ * min_batch = -1 (the default) selects B > 16 x CUs; 0 never.  cmpc_plan_heavy_first_batch
+ * returns the effective bound (0: never). */
+int cmpc_plan_set_heavy_first(cmpc_plan* plan, int64_t min_batch);
+int cmpc_plan_heavy_first_batch(const cmpc_plan* plan, int64_t* min_batch);
 
 /* Thread-local description of the last error returned on this thread ("" if none). */
 const char* cmpc_last_error(void);

@@ -76,6 +76,10 @@ def test_null_arguments(lib):
     assert "cmpc_leg_torque" in lib.cmpc_last_error().decode()
     assert lib.cmpc_srb_step(None, 1, 20, 0.001, *([None] * 5), 12, *([None] * 5)) == -22
     assert "cmpc_srb_step" in lib.cmpc_last_error().decode()
+    for name in ("cmpc_plan_set_team", "cmpc_plan_set_ipm", "cmpc_plan_set_heavy_first"):
+        assert getattr(lib, name)(None, -1) == -22
+        assert name in lib.cmpc_last_error().decode()
+    assert lib.cmpc_plan_heavy_first_batch(None, None) == -22
     lib.cmpc_plan_destroy(None)
 
 

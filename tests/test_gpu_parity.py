@@ -131,6 +131,25 @@ def test_deterministic(plan):
     assert np.array_equal(w1, w2) and np.array_equal(s1, s2) and np.array_equal(i1, i2)
 
 
+def test_class_order_independent():
+    """cmpc_plan_set_heavy_first: which register class is submitted first changes only where
+    and when each instance runs, never its result (one wave solves it, deterministically).
+    Both orders on a config-3 batch above the team bound, bitwise."""
+    from cmpc import Plan, SolverParams, solve_batch, synth
+    b = synth.make_config(3, B=8192)
+    p = Plan(SolverParams(max_batch=8192))
+    assert p.heavy_first_batch() > 0
+    out = []
+    for hmin in (0, 1):  # never / always
+        p.set_heavy_first(hmin)
+        assert p.heavy_first_batch() == hmin
+        out.append(solve_batch(b, plan=p))
+    p.set_heavy_first(-1)
+    (w0, s0, i0), (w1, s1, i1) = out
+    assert np.all(s0 == 1)
+    assert np.array_equal(w0, w1) and np.array_equal(s0, s1) and np.array_equal(i0, i1)
+
+
 def test_full_size_certified_sample(plan):
     """The full config-3 batch (65,536 trot + mixed, the headline workload) in one solve: every
     instance status 1 and feasible, X the rollout of U, and 512 instances stratified over the
