@@ -64,10 +64,6 @@ __device__ __forceinline__ float uniformf(float v) {
 
 // v[l] and v[l ^ 32] (resp. v[l ^ 16]) without address registers (gfx950 permlane swaps):
 // after the swap the two results hold the lane's own value and its partner's in some order
-#ifdef CMPC_SHFL_PAIRS
-__device__ __forceinline__ void pair32(float v, float& a, float& b) { a = v; b = __shfl_xor(v, 32, 64); }
-__device__ __forceinline__ void pair16(float v, float& a, float& b) { a = v; b = __shfl_xor(v, 16, 64); }
-#else
 __device__ __forceinline__ void pair32(float v, float& a, float& b) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
   a = __int_as_float(r[0]);
@@ -78,7 +74,6 @@ __device__ __forceinline__ void pair16(float v, float& a, float& b) {
   a = __int_as_float(r[0]);
   b = __int_as_float(r[1]);
 }
-#endif
 
 // max over the wave, result in every lane
 __device__ __forceinline__ float wave_max(float v) {
@@ -211,6 +206,26 @@ constexpr int kRefineExtra = 4;      // polish refinements beyond polish_refine 
 constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least this much
 constexpr int kBackoffCap = 3;       // polish back-off doubles per failed session, up to 8x
 constexpr int kLateRepairs = 3;      // repair budget of the sessions after two failed ones
+// Damped repairs (round 3).  A full primal-dual active-set step changes every violated triple
+// at once; on the slow instances the polished point then violates a different handful of
+// triples and the repairs wander between neighbouring face sets (traced on the NumPy model:
+// 34087 made 16 repairs over four sessions, each changing 2-8 triples, maximum relative
+// violation 0.02-1.0 throughout).  From the third repair of a session, and in every session
+// after a failed one, a repair changes only the most violated half of the triples it would
+// change (at least kRepairTop).  The first two repairs stay full steps, so an easy instance that
+// misses its first polish is untouched.  A/B in one gpurun call, two alternations: the N = 8
+// shard rehearsal 3.87 -> 2.99 ms, N = 4 5.18 -> 4.24 ms, config 2 at 8,192 3.72 -> 2.57 ms,
+// config 3 at 8,192 +8 %, config 2 at 65,536 +2 %, config 3 at 65,536 and config 2 at 4,096
+// unchanged; a fixed 2 (without the half) lost 35 % on config 2 at 4,096, a fixed 3 gained
+// nothing on the shards.
+#ifndef CMPC_REPAIR_TOP
+#define CMPC_REPAIR_TOP 2
+#endif
+constexpr int kRepairTop = CMPC_REPAIR_TOP;
+#ifndef CMPC_REPAIR_HALF
+#define CMPC_REPAIR_HALF 1
+#endif
+constexpr bool kRepairHalf = CMPC_REPAIR_HALF;
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
 constexpr float kLooseTol = 5.f;
@@ -785,11 +800,7 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
 #pragma unroll
         for (int J = 0; J <= I; ++J) {
           const int t = tile_index(I, J);
-#ifndef CMPC_EXP_INV_NO_MFMA
           M[t] = mfma4(a[I], b[J], M[t]);
-#else
-          M[t][0] += a[I] * b[J];
-#endif
         }
       }
       {  // -2 on the 4 pivot diagonals
@@ -1201,10 +1212,12 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
 // s.tcnt and `changed` says whether any face changed.  `loose` says whether every relative KKT
 // violation (multipliers against the gradient scale, forces against the force scale) is within
 // kLooseTol x polish_tol; the candidate forces are left in s.dl[3t .. 3t+2] for that case.
+// top > 0: the repair changes only the `top` triples with the largest relative violation (the
+// others keep their faces).
 template <int NC>
 __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
                                              const float* __restrict__ Bg, int ntri, float step,
-                                             bool& changed, bool& loose) {
+                                             bool& changed, bool& loose, int top = 0) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
   float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -1242,6 +1255,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   const float tol_d = P.polish_tol * gs, tol_p = P.polish_tol * us;
   bool ok = true;
   int nc = 0;
+  float v = 0.f;
   if (owns) {
     // KKT per triple; on a violation also derive the repaired face set (primal-dual
     // active-set step): drop faces with a negative multiplier, add violated faces
@@ -1256,9 +1270,8 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     if (!sy && fabsf(fy) > mu * fz + tol_p) { ok = false; nc |= (fy > 0.f) ? 8 : 16; }
     if (!zl && fz < fzmin - tol_p) { ok = false; nc |= 1; }
     if (!(isfinite(fx) && isfinite(fy) && isfinite(fz))) ok = false;
-    s.tcnt[lane] = nc;  // repaired code (copied into s.code by the caller if used)
     const float ig = 1.f / fmaxf(gs, 1e-30f), iu = 1.f / us;
-    float v = fmaxf(fmaxf(sx ? -lx * ig : 0.f, sy ? -ly * ig : 0.f), zl ? -l0 * ig : 0.f);
+    v = fmaxf(fmaxf(sx ? -lx * ig : 0.f, sy ? -ly * ig : 0.f), zl ? -l0 * ig : 0.f);
     v = fmaxf(v, fmaxf(sx ? 0.f : (fabsf(fx) - mu * fz) * iu, sy ? 0.f : (fabsf(fy) - mu * fz) * iu));
     v = fmaxf(v, zl ? 0.f : (fzmin - fz) * iu);
     const bool fin = isfinite(fx) && isfinite(fy) && isfinite(fz);
@@ -1267,6 +1280,24 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     s.dl[3 * lane + 1] = fy;
     s.dl[3 * lane + 2] = fz;
   }
+  if (top > 0) {  // uniform: keep the faces of all but the `top` most violated triples
+    const bool cand = owns && nc != code;
+    float key = cand ? (isfinite(v) ? v : INFINITY) : -1.f;  // a changed triple has v > 0
+    bool sel = false;
+    const int ncand = __popcll(__ballot(cand));
+    const int kk = kRepairHalf ? max(top, (ncand + 1) >> 1) : top;  // (uniform)
+    for (int r = 0; r < kk; ++r) {
+      const float m = wave_max(key);
+      if (!(m > 0.f)) break;  // uniform: no candidate left
+      const unsigned long long bal = __ballot(key == m);
+      if (lane == __builtin_ctzll(bal)) {
+        sel = true;
+        key = -1.f;
+      }
+    }
+    if (cand && !sel) nc = code;
+  }
+  if (owns) s.tcnt[lane] = nc;  // repaired code (copied into s.code by the caller if used)
   changed = __any(owns && nc != code) != 0;
   const bool step_ok = step <= P.polish_tol * us;
   loose = (__all(lok) != 0) && step_ok;
@@ -1947,7 +1978,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       }
       gradient<NC, (W > 1)>(s, P, nact, s.v, s.g, pwc, twc);  // E, L at the final point
       bool changed = false, loose = false;
-      const bool ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose);
+      // a hard instance's later repairs move only the worst triples: full primal-dual
+      // active-set steps swap several faces at a time and can wander between neighbouring sets
+      const int top = (kRepairTop > 0 && (nfail > 0 || ntried >= 3)) ? kRepairTop : 0;
+      const bool ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, top);
 #ifdef CMPC_TRACE
       if (b == CMPC_TRACE && lane == 0)
         printf("it %d polish nact %d ok %d loose %d changed %d step %g repairs_left %d\n", it, nact,

@@ -14,7 +14,9 @@ F32 = np.float32
 class Params:
     def __init__(self, N=16, Q=None, R=None, mu=0.8, fz_min=10.0, rho=1e-4, sigma=1e-6,
                  alpha=1.6, max_iter=400, stable_checks=3, adaptive_interval=25,
-                 eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=6):
+                 eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=6,
+                 fail_rho=4.0, late_repairs=3, backoff_cap=3, repair_top=2,
+                 repair_top_from=1, repair_top_rep=2, repair_frac=0.5):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -25,6 +27,11 @@ class Params:
         self.eps_abs, self.eps_rel = eps_abs, eps_rel
         self.polish_refine, self.tol_polish = polish_refine, tol_polish
         self.repairs = repairs
+        self.fail_rho, self.late_repairs, self.backoff_cap = fail_rho, late_repairs, backoff_cap
+        self.repair_top = repair_top  # >0: a repair changes only the triples of the top violations
+        self.repair_top_from = repair_top_from  # ... from the session after this many failed ones
+        self.repair_top_rep = repair_top_rep    # ... or from this repair of any session on
+        self.repair_frac = repair_frac          # ... at least this fraction of the changed triples
 
 
 def project(v, mu, fz_min):
@@ -215,11 +222,17 @@ def solve(inst, p: Params):
                         0.0 if c & 1 else (p.fz_min - fz) / us)
                 viol[ti] = v
                 ti += 1
+        if p.repair_top > 0 and (len(failed_starts) >= p.repair_top_from or cur_rep[0] >= p.repair_top_rep):
+            ncand = int(np.sum(newcode != code))
+            kk = max(p.repair_top, int(np.ceil(p.repair_frac * ncand)))
+            keep = np.argsort(-viol)[kk:]
+            newcode[keep] = code[keep]
         self_newcode[0] = newcode
         self_loose[0] = bool(step <= p.tol_polish * us) and bool(np.all(viol <= 5.0 * p.tol_polish))
         return ok, u
 
     self_newcode = [None]
+    cur_rep = [0]  # repairs made so far in the current session (repair_top_rep)
     self_loose = [False]
 
     failed_starts = []
@@ -250,7 +263,7 @@ def solve(inst, p: Params):
         else:
             stable = 0
         prev_code = code
-        backoff = p.stable_checks << min(len(failed_starts), 3)   # cmpc_wave.hip kBackoffCap
+        backoff = p.stable_checks << min(len(failed_starts), p.backoff_cap)   # cmpc_wave.hip kBackoffCap
         if stable >= p.stable_checks and it - last_pol >= backoff:
             last_pol = it
             # a session: polish ADMM's face set, then repair it.  A set that started a failed
@@ -259,17 +272,19 @@ def solve(inst, p: Params):
             start = code.tobytes()
             seen = start in failed_starts[-4:]
             tried = [start]
+            cur_rep[0] = 0
             ok, u = polish(z, code)
             rep = 0
-            budget = 0 if seen else (min(p.repairs, 3) if len(failed_starts) >= 2 else p.repairs)
+            budget = 0 if seen else (min(p.repairs, p.late_repairs) if len(failed_starts) >= 2 else p.repairs)
             while not ok and rep < budget:   # cmpc_wave.hip kLateRepairs
                 c2 = self_newcode[0]
                 if np.array_equal(c2, code) or c2.tobytes() in tried[:8]:
                     break
                 code = c2
                 tried.append(code.tobytes())
-                ok, u = polish(z, code)
                 rep += 1
+                cur_rep[0] = rep
+                ok, u = polish(z, code)
             stable = -backoff  # back off before the next attempt
             if not ok and self_loose[0]:
                 ok = True  # the session ends within the loose tolerance (kLooseTol): accepted
@@ -279,7 +294,7 @@ def solve(inst, p: Params):
                 failed_starts.append(start)
             if len(failed_starts) == 1 and not seen:
                 # the first failed session: continue at 4 x rho0 (cmpc_wave.hip kFailRho)
-                rho_low = False; rho = 4.0 * p.rho; L = admm_matrix(rho)
+                rho_low = False; rho = p.fail_rho * p.rho; L = admm_matrix(rho)
             elif rho_low:
                 rho_low = False; rho = p.rho; L = admm_matrix(rho)
         if p.adaptive_interval and it % p.adaptive_interval == 0:

@@ -23,7 +23,10 @@ def main():
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     # IPM_FACTS: the interior-point trigger (SolverParams.ipm_facts) for trigger sweeps
     facts = int(os.environ.get("IPM_FACTS", SolverParams.ipm_facts))
-    plan = Plan(SolverParams(max_batch=65536, ipm_facts=facts))
+    # CMPC_PARAMS="name=value,...": other SolverParams overrides (A/B of runtime parameters)
+    over = {k: type(getattr(SolverParams, k))(float(v)) for k, v in
+            (a.split("=") for a in os.environ.get("CMPC_PARAMS", "").split(",") if a)}
+    plan = Plan(SolverParams(max_batch=65536, ipm_facts=facts, **over))
     if os.environ.get("CMPC_IPM_BATCH"):  # kernel variants with the fallback up to this batch
         plan.set_ipm(int(os.environ["CMPC_IPM_BATCH"]))
     d = to_device_batch(synth.make_config(3))
