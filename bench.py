@@ -136,6 +136,8 @@ def parse(argv=None):
                     help="small-batch team mode for B <= this (cmpc_plan_set_team): -1 auto, 0 off")
     ap.add_argument("--ipm", type=int, default=int(os.environ.get("CMPC_IPM_BATCH", "-1")),
                     help="interior-point fallback kernels for B <= this (cmpc_plan_set_ipm): -1 auto")
+    ap.add_argument("--heavy-first", type=int, default=int(os.environ.get("CMPC_HEAVY_FIRST", "-1")),
+                    help="NC >= 160 class first for B >= this (cmpc_plan_set_heavy_first): -1 auto, 0 never")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     a = ap.parse_args(argv)
@@ -361,6 +363,8 @@ def main(argv=None):
         plan.set_team(args.team)
     if args.ipm != -1 and hasattr(plan.lib, "cmpc_plan_set_ipm"):
         plan.set_ipm(args.ipm)
+    if args.heavy_first != -1 and hasattr(plan.lib, "cmpc_plan_set_heavy_first"):
+        plan.set_heavy_first(args.heavy_first)
     stream = torch.cuda.current_stream(dev)
     d = to_device_batch(shard, dev)
     w = torch.empty((Bs, 24 * 16), dtype=torch.float32, device=dev)

@@ -222,6 +222,10 @@ constexpr int kLateRepairs = 3;      // repair budget of the sessions after two 
 #define CMPC_REPAIR_TOP 2
 #endif
 constexpr int kRepairTop = CMPC_REPAIR_TOP;
+#ifndef CMPC_STABLE_GROW
+#define CMPC_STABLE_GROW 1
+#endif
+constexpr int kStableGrow = CMPC_STABLE_GROW;
 #ifndef CMPC_REPAIR_HALF
 #define CMPC_REPAIR_HALF 1
 #endif
@@ -2159,7 +2163,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     // back off before a further attempt, longer after failed sessions: both the stable run and
     // the distance to the last session grow as polish_stable x 2^min(nfail, kBackoffCap)
     const int backoff = P.polish_stable << min(nfail, kBackoffCap);
-    if (stable >= P.polish_stable && !last && it - last_pol >= backoff &&
+    int need = P.polish_stable;  // (kStableGrow: the stable run required grows per failed session)
+    for (int f = 0; f < min(nfail, kBackoffCap); ++f) need *= kStableGrow;
+    if (stable >= need && !last && it - last_pol >= backoff &&
         (P.check_every == 1 || it % P.check_every == 0)) {  // (OPTS check_termination)
       do_pol = true;
       last_pol = it;

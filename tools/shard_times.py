@@ -27,6 +27,8 @@ def main():
     over = {k: type(getattr(SolverParams, k))(float(v)) for k, v in
             (a.split("=") for a in os.environ.get("CMPC_PARAMS", "").split(",") if a)}
     plan = Plan(SolverParams(**{"max_batch": 65536, "ipm_facts": facts, **over}))
+    if os.environ.get("CMPC_HEAVY_FIRST"):  # launch-order threshold (cmpc_plan_set_heavy_first)
+        plan.set_heavy_first(int(os.environ["CMPC_HEAVY_FIRST"]))
     if os.environ.get("CMPC_IPM_BATCH"):  # kernel variants with the fallback up to this batch
         plan.set_ipm(int(os.environ["CMPC_IPM_BATCH"]))
     d = to_device_batch(synth.make_config(3))
