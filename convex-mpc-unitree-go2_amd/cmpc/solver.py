@@ -39,7 +39,7 @@ class SolverParams:
     polish_refine: int = 4
     polish_tol: float = 1e-5
     polish_repairs: int = 6
-    ipm_facts: int = 8
+    ipm_facts: int = 0
     check_termination: int = 1   # OPTS check_termination (reference: 10; include/cmpc.h)
     max_batch: int = 65536
 

@@ -127,7 +127,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_refine = 4;
   p->polish_tol = 1e-5f;
   p->polish_repairs = 6;
-  p->ipm_facts = 8;
+  p->ipm_facts = 0;  // opt-in since the damped repairs
   p->check_termination = 1;  // (reference OPTS: 10, accepted; see include/cmpc.h)
   p->max_batch = 65536;
 }

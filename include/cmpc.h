@@ -79,7 +79,10 @@ typedef struct cmpc_params {
                              and re-polish) before resuming ADMM */
   int32_t ipm_facts;      /* an instance that has failed a polish session and spent this many
                              factorizations identifies its face set by interior-point steps
-                             (hard instances); 0 = never.  Default 8 */
+                             (hard instances); 0 = never.  Default 0: with the
+                             damped repairs the variants without the fallback are faster on
+                             every measured batch (config 3 at 8,192 2.86 -> 2.25 ms); 8 was
+                             the default before them */
   int32_t check_termination; /* ADMM iterations between termination tests (OPTS check_termination,
                              centroidal_mpc.py:31): the polish trigger (face set stable for
                              polish_stable iterations -> active-set polish + KKT check, the only
@@ -266,12 +269,12 @@ const char* cmpc_plan_solve_kernel(const cmpc_plan* plan, int64_t B, int k);
 int cmpc_plan_set_team(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
 
-/* Tail-bound batches.  A batch of B <= max_batch instances (one wave per QP, i.e. above the
- * small-batch bound) runs the kernel variants that carry the interior-point fallback for hard
- * instances (cmpc_params.ipm_facts): a small batch or an N-GPU shard takes as long
- * as its slowest instance, which the fallback shortens 2-3x.  Large batches run the variants
- * without it (its code costs registers on the hot path).  max_batch = -1 (the default) selects
- * B <= 64 x CUs; 0 never.  cmpc_plan_ipm_batch returns the effective bound. */
+/* Tail-bound batches.  When cmpc_params.ipm_facts > 0 (opt-in), a batch of B <= max_batch
+ * instances (one wave per QP, i.e. above the small-batch bound) runs the kernel variants that
+ * carry the interior-point fallback for hard instances: a small batch or an N-GPU
+ * shard takes as long as its slowest instance.  Large batches run the variants without it (its
+ * code costs registers on the hot path).  max_batch = -1 (the default) selects B <= 64 x CUs;
+ * 0 never.  cmpc_plan_ipm_batch returns the effective bound. */
 int cmpc_plan_set_ipm(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_ipm_batch(const cmpc_plan* plan, int64_t* max_batch);
 

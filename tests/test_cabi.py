@@ -41,7 +41,7 @@ def test_defaults_are_reference_constants(lib):
     assert abs(p.mu - 0.8) < 1e-7 and p.fz_min == 10.0                   # :15, :127
     assert abs(p.eps_abs - 1e-4) < 1e-9 and p.max_iter == 1000           # :25-27
     assert p.adaptive_rho_interval == 25                                 # :32
-    assert p.ipm_facts == 8  # interior-point fallback for hard instances
+    assert p.ipm_facts == 0  # interior-point fallback for hard instances: opt-in
     assert p.check_termination == 1  # OPTS check_termination (:31 has 10; include/cmpc.h says why)
     assert ctypes.sizeof(_lib.CParams) == 176  # include/cmpc.h layout (int64 max_batch at 168)
     assert _lib.CParams.max_batch.offset == 168

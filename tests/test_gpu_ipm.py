@@ -1,8 +1,9 @@
 """GPU parity of the interior-point face-set identification (cmpc_wave.hip ipm_identify,
 DESIGN.md 4h) against the KKT-certified optimum.
 
-The default plan runs it only on the few hard instances of tail-bound batches (B <= 64 x CUs,
-cmpc_plan_set_ipm; a failed polish session and 8 factorizations).  These tests force it early (ipm_facts = 1: after the first failed session)
+It is opt-in (cmpc_params.ipm_facts > 0; then on the hard instances of tail-bound batches,
+B <= 64 x CUs, cmpc_plan_set_ipm).  These tests force it early (ipm_facts = 1: after the first
+failed session)
 so that every instance whose first polish session fails -- ~1-2 % of config 2 / 3 -- goes
 through the interior-point steps, the polish session they start and, when that fails, the
 restored ADMM state.  Tolerance as in test_gpu_parity.py: max |U - U*| / max |U*| <= 1e-4.
