@@ -16,7 +16,7 @@ class Params:
                  alpha=1.6, max_iter=400, stable_checks=3, adaptive_interval=25,
                  eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=6,
                  fail_rho=4.0, late_repairs=3, backoff_cap=3, repair_top=2,
-                 repair_top_from=1, repair_top_rep=2, repair_frac=0.5, stable_grow=1):
+                 repair_top_from=1, repair_top_rep=2, repair_frac=0.5, stable_grow=3):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -265,7 +265,7 @@ def solve(inst, p: Params):
             stable = 0
         prev_code = code
         backoff = p.stable_checks << min(len(failed_starts), p.backoff_cap)   # cmpc_wave.hip kBackoffCap
-        if stable >= p.stable_checks * p.stable_grow ** len(failed_starts) and it - last_pol >= backoff:
+        if stable >= p.stable_checks * p.stable_grow ** min(len(failed_starts), p.backoff_cap) and it - last_pol >= backoff:
             last_pol = it
             # a session: polish ADMM's face set, then repair it.  A set that started a failed
             # session before is polished once more without repairs; a repair that returns to a
