@@ -232,6 +232,13 @@ constexpr int kRepairTop = CMPC_REPAIR_TOP;
 #define CMPC_STABLE_GROW 3
 #endif
 constexpr int kStableGrow = CMPC_STABLE_GROW;
+// The NC >= 160 bins also start at rho0 / 2 (round 3; NumPy model: -2.6 % cost in those bins).
+// A/B in one gpurun call, two alternations: config 3 at 65,536 11.43 -> 11.26 ms, config 2 at
+// 65,536 14.05 -> 13.67 ms, at 4,096 2.05 -> 1.95 ms, N = 8 shard rehearsal 2.51 -> 2.38 ms.
+#ifndef CMPC_RHO_LOW_HEAVY
+#define CMPC_RHO_LOW_HEAVY 1
+#endif
+constexpr bool kRhoLowHeavy = CMPC_RHO_LOW_HEAVY;
 #ifndef CMPC_REPAIR_HALF
 #define CMPC_REPAIR_HALF 1
 #endif
@@ -1798,12 +1805,13 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   if constexpr (kPow) gradient_powers(s, pw_c, tw_c);
   const f4* pwc = kPow ? pw_c : nullptr;
   const f4* twc = kPow ? tw_c : nullptr;
-  // initial rho per bin: the NC = 128 bin (33-42 stance triples, trot-like schedules) converges
-  // in fewer iterations from rho0 / 2; its hard instances (a failed polish session) go back to
-  // rho0, where they converge as before (cfg1 +6-10 %, cfg2 +1 %; rho0 / 2 for every bin loses
-  // 7 % on cfg2)
-  float rho = (NC == 128) ? 0.5f * P.rho0 : P.rho0;
-  bool rho_low = NC == 128;  // still at the bin's reduced initial rho
+  // initial rho per bin: the NC >= 128 bins (33-64 stance triples) converge in fewer iterations
+  // from rho0 / 2; their hard instances (a failed polish session) go back to rho0, where they
+  // converge as before (NC = 128: cfg1 +6-10 %, cfg2 +1 %; NC >= 160: kRhoLowHeavy; rho0 / 2
+  // for the NC = 96 bin too loses 7 % on cfg2)
+  constexpr bool kLow = (NC == 128) || (kRhoLowHeavy && NC > 128);
+  float rho = kLow ? 0.5f * P.rho0 : P.rho0;
+  bool rho_low = kLow;  // still at the bin's reduced initial rho
   if (!resume) s.pcode[lane] = -1;
   if (resume) {
   } else if (in.w_init == nullptr && in.y_init == nullptr && in.lam_init == nullptr) {

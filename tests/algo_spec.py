@@ -237,9 +237,9 @@ def solve(inst, p: Params):
     self_loose = [False]
 
     failed_starts = []
-    # the NC = 128 bin (96 < nf <= 128) starts from rho / 2 and returns to rho after its first
+    # the NC >= 128 bins (nf > 96) start from rho / 2 and return to rho after their first
     # failed polish session (cmpc_wave.hip solve_instance, rho_low)
-    rho_low = 96 < nf <= 128
+    rho_low = nf > 96
     rho = p.rho * (0.5 if rho_low else 1.0)
     L = admm_matrix(rho)
     x = np.zeros(nf, F32); z = np.zeros(nf, F32); y = np.zeros(nf, F32)
