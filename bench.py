@@ -20,7 +20,7 @@ Also on the line:
   * ``weak``: every rank solves the whole 65,536-instance batch (per-GPU work fixed);
   * ``configs`` (N = 1): BASELINE configs 1 (B = 256) and 2 (B = 4,096), plus configs 1 and 2
     at B = 65,536, each timed the same way with its own roofline;
-  * ``roofline``: the dominant solve kernel (of the two, cmpc_host.hip) priced against HBM:
+  * ``roofline``: the dominant solve kernel (of the three, cmpc_host.hip) priced against HBM:
     12,264 algorithmic bytes per solve (inputs 10,720 + outputs 1,544) x the solves it
     processed / its average HIP-event duration on its own stream; ``traffic`` = the PMC HBM
     bytes per launch from profiles/;
@@ -54,8 +54,7 @@ HBM_PEAK_GBS = 8000.0                            # MI355X_MICROARCH.md: 8.0 TB/s
 F32_MATRIX_PEAK_TFS = 157.3                      # MI355X_MICROARCH.md: dense f32 MFMA peak
 POLISH_REFINE = 4                                # SolverParams.polish_refine (default)
 GLOBAL_BATCH = {1: 256, 2: 4096, 3: 65536}       # BASELINE.json configs[1..3]
-# solve kernels of builds without cmpc_plan_solve_kernel (two register-class kernels)
-KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<192, 160>")
+from cmpc._lib import BIN_CAPS, KERNEL_BINS, KERNEL_NAMES  # noqa: E402  (no GPU touched)
 
 
 def algorithmic_flops(contact, iters, N=16):
@@ -77,15 +76,17 @@ def algorithmic_flops(contact, iters, N=16):
     return 2.0 * (cond + inv) + it * (symv + grad) + POLISH_REFINE * symv + (POLISH_REFINE + 1) * grad
 
 
-def bins_of(contact):
+def bins_of(contact, caps=BIN_CAPS):
     nf = 3 * (contact != 0).reshape(contact.shape[0], -1).sum(1)
-    caps = np.array([96, 128, 160, 192])
-    return np.searchsorted(caps, nf)   # first cap >= nf
+    return np.searchsorted(np.asarray(caps), nf)   # first cap >= nf
 
 
-def kernel_of_bins(bins):
+def kernel_of_bins(bins, kernel_bins=KERNEL_BINS):
+    """Solve kernel (timing slot) of each instance's bin (cmpc_host.hip group_first_bin)."""
     k = np.zeros_like(bins)
-    k[bins >= 2] = 1
+    for kk, bs in enumerate(kernel_bins):
+        for b in bs:
+            k[bins == b] = kk
     return k
 
 
@@ -229,16 +230,18 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
     With PMC counters in profiles/, the compute roofline is the counted MFMA work over the live
     duration; `step` prices every launched kernel together over the whole step."""
     names = plan.solve_kernels(B_shard)
-    if names[0] is None:  # an older A/B build without cmpc_plan_solve_kernel: two class kernels
+    if names[0] is None:  # an older A/B build without cmpc_plan_solve_kernel
         names = list(KERNEL_NAMES)
-    kern = kernel_of_bins(bins) if names[1] is not None else np.zeros_like(bins)
-    nk = 2 if names[1] is not None else 1
-    avg = [ms[k] / max(calls[k], 1) for k in range(2)]
-    n_k = [int(np.sum(kern == k)) for k in range(2)]
-    q = int(np.argmax(n_k[:nk]))                 # dominant: most solves
-    c = int(np.argmax(avg[:nk]))                 # critical: longest live time
-    flops = algorithmic_flops(contact, iters)
     team = names[0].startswith("solve_team")
+    nk = len(names)
+    live = [k for k in range(nk) if names[k] is not None]
+    # one launched kernel (team mode, or a build with one kernel for every bin) solves them all
+    kern = np.zeros_like(bins) if len(live) == 1 else kernel_of_bins(bins)
+    avg = [ms[k] / max(calls[k], 1) for k in range(nk)]
+    n_k = [int(np.sum(kern == k)) for k in range(nk)]
+    q = max(live, key=lambda k: n_k[k])          # dominant: most solves
+    c = max(live, key=lambda k: avg[k])          # critical: longest live time
+    flops = algorithmic_flops(contact, iters)
 
     def hbm(k):
         achieved = BYTES_PER_SOLVE * n_k[k] / (avg[k] * 1e-3) / 1e9 if avg[k] > 0 else 0.0
@@ -268,8 +271,8 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
         return comp
 
     roof = hbm(q)
-    roof.update(kernel_avg_ms_all={names[k]: avg[k] for k in range(nk)},
-                solves_per_kernel={names[k]: n_k[k] for k in range(nk)})
+    roof.update(kernel_avg_ms_all={names[k]: avg[k] for k in live},
+                solves_per_kernel={names[k]: n_k[k] for k in live})
     comp = compute(q)
     crit = hbm(c)
     crit["compute"] = compute(c)
@@ -277,11 +280,11 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
     crit["same_as_dominant"] = c == q
     if step_ms and not team:
         # every launched solve kernel together over the step
-        mf = [(_counters_of(counters, names[k]) or {}).get("SQ_INSTS_MFMA") for k in range(nk)]
-        st = {"step_ms": step_ms, "solves": int(sum(n_k[:nk])),
-              "hbm_achieved_GBs": BYTES_PER_SOLVE * sum(n_k[:nk]) / (step_ms * 1e-3) / 1e9}
+        mf = [(_counters_of(counters, names[k]) or {}).get("SQ_INSTS_MFMA") for k in live]
+        st = {"step_ms": step_ms, "solves": int(sum(n_k[k] for k in live)),
+              "hbm_achieved_GBs": BYTES_PER_SOLVE * sum(n_k[k] for k in live) / (step_ms * 1e-3) / 1e9}
         st["hbm_frac"] = st["hbm_achieved_GBs"] / HBM_PEAK_GBS
-        if all(m for m, k in zip(mf, range(nk)) if n_k[k] > 0) and any(mf):
+        if all(m for m, k in zip(mf, live) if n_k[k] > 0) and any(mf):
             tf = sum(m for m in mf if m) * 2048.0 / (step_ms * 1e-3) / 1e12
             st.update(mfma_achieved_TFs=tf, mfma_frac=tf / F32_MATRIX_PEAK_TFS,
                       mfma_basis="SQ_INSTS_MFMA of the launched kernels (profiles/ counters)")
@@ -526,7 +529,7 @@ def main(argv=None):
             "iters_mean": float(np.mean(iters)),
             "iters_max": int(np.max(iters)),
             "status_counts": {str(s): int(np.sum(status == s)) for s in np.unique(status)},
-            "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate((96, 128, 160, 192))},
+            "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate(BIN_CAPS)},
             "scatter_gather": scat,
             "weak": weak,
             "configs": configs,

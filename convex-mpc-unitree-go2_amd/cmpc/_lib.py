@@ -7,11 +7,13 @@ The product path has no CPU fallback: if the library is missing this module rais
 from __future__ import annotations
 
 import ctypes
+import os
 from pathlib import Path
 
 from .build import LIB
 
-ABI_VERSION = 3
+ABI_VERSION = 4
+ABI_COMPAT = (3, 4)   # cmpc_params layouts identical to this one (A/B builds of earlier rounds)
 CMPC_OK = 0
 
 
@@ -46,21 +48,26 @@ EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_d
            "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch", "cmpc_plan_set_heavy_first",
            "cmpc_plan_heavy_first_batch", "cmpc_plan_solve_kernel", "cmpc_last_error",
            "cmpc_version")
-NUM_BINS = 4
-BIN_CAPS = (96, 128, 160, 192)
-# solve kernels (register classes): 0 = bins NC 128 + 96, 1 = bins NC 192 + 160
-NUM_SOLVE_KERNELS = 2
-KERNEL_BINS = ((1, 0), (3, 2))
-KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<192, 160>")
+NUM_BINS = 5
+BIN_CAPS = (96, 128, 144, 160, 192)
+# solve kernels (timing slots): 0 = bins NC 128 + 96 (two waves per SIMD), 1 = bins NC 160 + 144,
+# 2 = bin NC 192 (one wave per SIMD each)
+NUM_SOLVE_KERNELS = 3
+KERNEL_BINS = ((1, 0), (3, 2), (4,))
+KERNEL_NAMES = ("solve_group_kernel<128, 96>", "solve_group_kernel<160, 144>",
+                "solve_group_kernel<192, 0>")
 
 _lib = None
 
 
 def load(path: str | Path | None = None) -> ctypes.CDLL:
-    """Load libcmpc.so (in-tree) and declare the prototypes.  Raises if it is missing."""
+    """Load libcmpc.so (in-tree; $CMPC_LIB names a variant build, e.g. the one with the
+    interior-point fallback) and declare the prototypes.  Raises if it is missing."""
     global _lib
     if _lib is not None and path is None:
         return _lib
+    if path is None and os.environ.get("CMPC_LIB"):
+        path = os.environ["CMPC_LIB"]
     p = Path(path) if path is not None else LIB
     if not p.exists():
         raise RuntimeError(f"cmpc: HIP library {p} not built (run __graft_entry__.build() or "

@@ -96,6 +96,10 @@ class Plan:
         with torch.cuda.device(self.device):
             h = ctypes.c_void_p()
             cp = self.params.to_c()
+            d = _lib.CParams()
+            self.lib.cmpc_params_default(ctypes.byref(d))
+            if d.abi_version in _lib.ABI_COMPAT:  # (an earlier round's A/B build, same layout)
+                cp.abi_version = d.abi_version
             _check(self.lib, self.lib.cmpc_plan_create(ctypes.byref(cp), ctypes.byref(h)),
                    "cmpc_plan_create")
         self._h = h
@@ -148,13 +152,13 @@ class Plan:
         return int(v.value)
 
     def set_heavy_first(self, min_batch: int):
-        """Submit the NC >= 160 register class first for solves of B >= min_batch: -1 =
+        """Submit the NC 144 / 160 register class first for solves of B >= min_batch: -1 =
         automatic (B > 16 x CUs, the default), 0 = never (cmpc_plan_set_heavy_first)."""
         _check(self.lib, self.lib.cmpc_plan_set_heavy_first(self._h, int(min_batch)),
                "cmpc_plan_set_heavy_first")
 
     def heavy_first_batch(self) -> int:
-        """The smallest batch that submits the NC >= 160 class first, 0 = never
+        """The smallest batch that submits the NC 144 / 160 class first, 0 = never
         (cmpc_plan_heavy_first_batch)."""
         v = ctypes.c_int64()
         _check(self.lib, self.lib.cmpc_plan_heavy_first_batch(self._h, ctypes.byref(v)),
@@ -173,8 +177,8 @@ class Plan:
         return out
 
     def timing_read(self):
-        """-> (ms_per_kernel[2], calls_per_kernel[2]) of the two solve kernels since the last
-        read (kernel 0: bins NC 128 + 96; kernel 1: bins NC 192 + 160, _lib.KERNEL_BINS)."""
+        """-> (ms_per_kernel, calls_per_kernel) of the solve kernels since the last read, one
+        entry per timing slot (_lib.KERNEL_BINS: 0 = NC 128 + 96, 1 = NC 160 + 144, 2 = NC 192)."""
         ms = (ctypes.c_float * 4)()       # room for the round-1 ABI's four slots (A/B builds)
         calls = (ctypes.c_int32 * 4)()
         _check(self.lib, self.lib.cmpc_plan_timing_read(self._h, ms, calls),

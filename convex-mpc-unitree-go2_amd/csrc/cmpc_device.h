@@ -44,8 +44,11 @@ struct Outputs {
   float* lam;           // nullable: the reference's multipliers [B][52N] = [lam_x | lam_a]
 };
 
-// Free-variable capacities of the LDS bins (3 forces per stance (step, leg)).
-constexpr int kNumBins = 4;
-constexpr int kBinCap[kNumBins] = {96, 128, 160, 192};
+// Free-variable capacities of the LDS bins (3 forces per stance (step, leg)).  Solve kernels
+// (register classes, cmpc_wave.hip solve_group_kernel): bins 1 + 0 (NC 128, 96: two waves per
+// SIMD), bins 3 + 2 (NC 160, 144: one wave per SIMD), bin 4 (NC 192: one wave per SIMD, its own
+// kernel so that the rare > 160 instances do not size the NC <= 160 kernel's registers).
+constexpr int kNumBins = 5;
+constexpr int kBinCap[kNumBins] = {96, 128, 144, 160, 192};
 
 }  // namespace cmpc

@@ -19,7 +19,8 @@
 #include "cmpc_leg.hip"       // leg controller (stance torque mapping, swing) kernel
 #include "cmpc_sim.hip"       // single-rigid-body plant (closed-loop stand-in for MuJoCo)
 
-constexpr int kNumGroups = 2;  // solve kernels (register classes), see solve_group_kernel
+constexpr int kNumGroups = 3;  // solve kernels (register classes), see solve_group_kernel
+static_assert(kNumGroups == CMPC_NUM_SOLVE_KERNELS, "one timing slot per solve kernel");
 
 struct cmpc_plan {
   cmpc_params p;
@@ -42,13 +43,16 @@ struct cmpc_plan {
   int64_t ipm_max_batch = -1;   // -1: automatic (B <= 64 x CUs)
   // batches of B >= heavy_first_min_batch submit the NC >= 160 class first
   int64_t heavy_first_min_batch = -1;  // -1: automatic (B > 16 x CUs), 0: never
-  // The two solve kernels (one per register class, cmpc_wave.hip solve_group_kernel) run
-  // concurrently, one on the caller's stream (submitted first) and one on a plan stream forked
-  // from / joined to it.  Two streams in total stay within the device's hardware queues
-  // (GPU_MAX_HW_QUEUES = 4), so the classes overlap instead of sharing a queue.
+  // The solve kernels (cmpc_wave.hip solve_group_kernel: the NC <= 128 class, the NC 144 / 160
+  // class, the NC 192 bin) run concurrently: one class on the caller's stream, the other on a
+  // plan stream, the NC 192 kernel on a second plan stream, both forked from / joined to the
+  // caller's.  Three streams in total stay within the device's hardware queues
+  // (GPU_MAX_HW_QUEUES = 4), so the kernels overlap instead of sharing a queue.
   hipStream_t side = nullptr;
+  hipStream_t top = nullptr;
   hipEvent_t fork = nullptr;
   hipEvent_t join = nullptr;
+  hipEvent_t join_top = nullptr;
   // timing hooks
   bool timing = false;
   struct Rec { hipEvent_t a, b; int group; };
@@ -82,22 +86,53 @@ int check_device(const cmpc_plan* pl, const char* what) {
   return CMPC_OK;
 }
 
-// group 0: bins 1 (NC 128) then 0 (NC 96), two waves per SIMD; group 1: bins 3 (NC 192) then
-// 2 (NC 160), one wave per SIMD.  qa = the group's first (larger) bin.
-int group_first_bin(int k) { return k == 0 ? 1 : 3; }
+// group 0: bins 1 (NC 128) then 0 (NC 96), two waves per SIMD; group 1: bins 3 (NC 160) then
+// 2 (NC 144), one wave per SIMD; group 2: bin 4 (NC 192) alone, one wave per SIMD.  qa = the
+// group's first (larger) bin.
+int group_first_bin(int k) { return k == 0 ? 1 : (k == 1 ? 3 : 4); }
 
 constexpr int kTeamWaves = 4;
 
+// The kernel variants carrying the interior-point fallback are compiled only with
+// -DCMPC_WITH_IPM (scripts/build_variant.sh ipm -DCMPC_WITH_IPM): no measured batch gains from
+// them since the damped repairs, and the default library keeps only the kernels that run.
+#ifdef CMPC_WITH_IPM
+constexpr bool kHasIpm = true;
+#else
+constexpr bool kHasIpm = false;
+#endif
+
 KernelFn group_fn(int k, bool ipm = false) {
+#ifdef CMPC_WITH_IPM
   if (ipm)
-    return k == 0 ? cmpc::solve_group_kernel<128, 96, true> : cmpc::solve_group_kernel<192, 160, true>;
-  return k == 0 ? cmpc::solve_group_kernel<128, 96, false> : cmpc::solve_group_kernel<192, 160, false>;
+    return k == 0 ? cmpc::solve_group_kernel<128, 96, true>
+                  : (k == 1 ? cmpc::solve_group_kernel<160, 144, true> : cmpc::solve_group_kernel<192, 0, true>);
+#else
+  (void)ipm;
+#endif
+  return k == 0 ? cmpc::solve_group_kernel<128, 96, false>
+                : (k == 1 ? cmpc::solve_group_kernel<160, 144, false> : cmpc::solve_group_kernel<192, 0, false>);
+}
+
+const char* group_name(int k, bool ipm) {
+  static const char* names[2][kNumGroups] = {
+      {"solve_group_kernel<128, 96, false>", "solve_group_kernel<160, 144, false>",
+       "solve_group_kernel<192, 0, false>"},
+      {"solve_group_kernel<128, 96, true>", "solve_group_kernel<160, 144, true>",
+       "solve_group_kernel<192, 0, true>"}};
+  return names[ipm ? 1 : 0][k];
 }
 
 // park slab per wave (floats): the one-wave inverse (+ the interior-point state)
 size_t group_slab(int k) {
   return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
-                : std::max(cmpc::Cfg<192>::SLAB, cmpc::Cfg<160>::SLAB);
+                : (k == 1 ? std::max(cmpc::Cfg<160>::SLAB, cmpc::Cfg<144>::SLAB) : cmpc::Cfg<192>::SLAB);
+}
+
+// which solve kernels a horizon can need: the NC >= 144 class once the horizon can hold more
+// than 128 free forces, the NC 192 kernel once more than 160
+bool has_group(const cmpc_plan* pl, int k) {
+  return k == 0 || cmpc::kBinCap[k == 1 ? 1 : 3] < 12 * pl->kp.N;
 }
 
 }  // namespace
@@ -154,6 +189,9 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     return fail(CMPC_E_INVALID, "cmpc_plan_create: polish settings out of range");
   if (p->adaptive_rho_interval < 0 || p->max_batch < 1 || p->max_batch > (1LL << 30))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: adaptive_rho_interval/max_batch out of range");
+  if (!kHasIpm && p->ipm_facts > 0)
+    return fail(CMPC_E_INVALID, "cmpc_plan_create: ipm_facts > 0 needs a library built with "
+                                "-DCMPC_WITH_IPM (the interior-point fallback is not in this build)");
 
   cmpc_plan* pl = new cmpc_plan();
   pl->p = *p;
@@ -190,7 +228,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   size_t work_floats = 0;
   for (int k = 0; k < kNumGroups; ++k) {
     int nb = 1 << 30;
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < (kHasIpm ? 2 : 1); ++v) {
       int b = 0;
       e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, group_fn(k, v == 1), 64, 0);
       if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
@@ -235,8 +273,10 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
   if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&pl->top, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&pl->join, hipEventDisableTiming)) != hipSuccess) {
+      (e = hipEventCreateWithFlags(&pl->join, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&pl->join_top, hipEventDisableTiming)) != hipSuccess) {
     cmpc_plan_destroy(pl);
     return hip_fail(e, "side stream/event creation");
   }
@@ -326,6 +366,8 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
 }
 
 static int64_t heavy_first_batch(const cmpc_plan* pl) {
+  // (0 = never: also when the horizon is too short for an NC >= 144 class to exist)
+  if (!has_group(pl, 1)) return 0;
   return pl->heavy_first_min_batch >= 0 ? pl->heavy_first_min_batch : 16LL * pl->cus + 1;
 }
 
@@ -373,7 +415,7 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
   // tail-bound batch: the kernel variants with the interior-point fallback
-  const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
+  const bool ipm = kHasIpm && pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
   if (B <= 1024) {  // one workgroup bins the batch and zeroes the queue heads (no memset)
     hipLaunchKernelGGL(cmpc::bin_small_kernel, dim3(1), dim3(1024), 0, st, pl->kp.N, (int)B,
                        in.contact, pl->d_counters, pl->d_counters + cmpc::kNumBins, pl->d_lists,
@@ -406,24 +448,40 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // (config 2 at 4,096: 2.0 vs 2.4 ms) keep the NC <= 128 class first.  Heavy-first relies on
   // the LDS slot padding of solve_group_kernel (cmpc_wave.hip kLdsSlot): without it the
   // NC <= 128 waves that replace the NC >= 160 ones fit ~6 instead of 8 per CU.
-  const bool big = cmpc::kBinCap[1] < 12 * pl->kp.N;
+  // The NC 192 bin (rare: one instance in config 3's 65,536) has its own kernel on the second
+  // plan stream, submitted before the classes so that its waves -- which exit at once when the
+  // bin is empty -- are dispatched before the classes fill the SIMDs, and its instances start
+  // at the beginning of the step (a one-wave-per-SIMD wave could not start later, with the
+  // SIMDs held by two-wave NC <= 128 waves).
+  const bool big = has_group(pl, 1), top = has_group(pl, 2);
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(pl->side, pl->fork, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
+    if (top && (e = hipStreamWaitEvent(pl->top, pl->fork, 0)) != hipSuccess)
+      return hip_fail(e, "hipStreamWaitEvent");
   }
-  const unsigned g0 = (unsigned)(pl->grid[0] < B ? pl->grid[0] : B);
-  const unsigned g1 = (unsigned)(pl->grid[1] < B ? pl->grid[1] : B);
+  unsigned gk[kNumGroups];
+  for (int k = 0; k < kNumGroups; ++k) gk[k] = (unsigned)(pl->grid[k] < B ? pl->grid[k] : B);
+  if (top) {
+    rc = record_launch(pl, 2, pl->top, kp, in, out, gk[2], ipm);
+    if (rc != CMPC_OK) return rc;
+  }
   const int64_t hmin = heavy_first_batch(pl);
   const int first = (big && hmin > 0 && B >= hmin) ? 1 : 0;  // class submitted first
-  rc = record_launch(pl, first, st, kp, in, out, first ? g1 : g0, ipm);
+  rc = record_launch(pl, first, st, kp, in, out, gk[first], ipm);
   if (rc != CMPC_OK) return rc;
   if (big) {
-    rc = record_launch(pl, 1 - first, pl->side, kp, in, out, first ? g0 : g1, ipm);
+    rc = record_launch(pl, 1 - first, pl->side, kp, in, out, gk[1 - first], ipm);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
+    if (top) {
+      if ((e = hipEventRecord(pl->join_top, pl->top)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+      if ((e = hipStreamWaitEvent(st, pl->join_top, 0)) != hipSuccess)
+        return hip_fail(e, "hipStreamWaitEvent");
+    }
   }
   return CMPC_OK;
 }
@@ -572,10 +630,9 @@ int cmpc_plan_heavy_first_batch(const cmpc_plan* pl, int64_t* min_batch) {
 const char* cmpc_plan_solve_kernel(const cmpc_plan* pl, int64_t B, int k) {
   if (!pl || B < 1 || k < 0 || k >= kNumGroups) return nullptr;
   if (B <= team_batch(pl)) return k == 0 ? "solve_team_kernel<4>" : nullptr;
-  const bool ipm = pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
-  if (k == 1 && !(cmpc::kBinCap[1] < 12 * pl->kp.N)) return nullptr;
-  if (k == 0) return ipm ? "solve_group_kernel<128, 96, true>" : "solve_group_kernel<128, 96, false>";
-  return ipm ? "solve_group_kernel<192, 160, true>" : "solve_group_kernel<192, 160, false>";
+  const bool ipm = kHasIpm && pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
+  if (!has_group(pl, k)) return nullptr;
+  return group_name(k, ipm);
 }
 
 int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_kernel, int32_t* calls_per_kernel) {
@@ -601,8 +658,10 @@ void cmpc_plan_destroy(cmpc_plan* pl) {
   for (auto& r : pl->recs) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   for (auto& r : pl->pool) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
   if (pl->side) (void)hipStreamDestroy(pl->side);
+  if (pl->top) (void)hipStreamDestroy(pl->top);
   if (pl->fork) (void)hipEventDestroy(pl->fork);
   if (pl->join) (void)hipEventDestroy(pl->join);
+  if (pl->join_top) (void)hipEventDestroy(pl->join_top);
   (void)hipFree(pl->d_counters);
   (void)hipFree(pl->d_lists);
   (void)hipFree(pl->d_work);

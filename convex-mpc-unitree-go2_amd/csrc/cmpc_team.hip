@@ -32,9 +32,10 @@ struct TeamCfg {
   static constexpr int TT = NC / 16;
   static constexpr int NPAIR = TT / 2;
   static constexpr int PPW = (NPAIR + W - 1) / W;  // column pairs per wave
-  static constexpr int SLOTS = PPW * (TT + 1);     // register tiles per wave
+  // register tiles per wave (W = 1: the one-wave kernels, every lower tile)
+  static constexpr int SLOTS = W == 1 ? TT * (TT + 1) / 2 : PPW * (TT + 1);
   static constexpr int SLAB = W * SLOTS * 256;     // park slab of the team (floats)
-  static_assert(TT % 2 == 0, "team mode pairs tile columns");
+  static_assert(W == 1 || TT % 2 == 0, "team mode pairs tile columns");
 };
 
 enum : int { kOpExit = 0, kOpFactor = 1, kOpSymv = 2, kOpParkStore = 3, kOpParkLoad = 4 };
@@ -692,7 +693,7 @@ __device__ __forceinline__ void team_symv_lead(Smem<NC>& s, TeamSmem<NC, W>& ts,
 }
 
 // helpers 1..W-1, each with its wave index as a compile-time constant; they follow the leader
-// through the four bins (heaviest first, as solve_team_kernel drains them)
+// through the five bins (heaviest first, as solve_team_kernel drains them)
 template <int W, int WV>
 __device__ __forceinline__ void team_helpers(Smem<192>& s3, TeamSmem<192, W>& t3, Smem<160>& s2,
                                              TeamSmem<160, W>& t2, Smem<128>& s1,
@@ -702,7 +703,8 @@ __device__ __forceinline__ void team_helpers(Smem<192>& s3, TeamSmem<192, W>& t3
   if constexpr (WV < W) {
     if (w == WV) {
       team_helper<192, W, WV>(s3, t3, P, park, seq);
-      team_helper<160, W, WV>(s2, t2, P, park, seq);
+#pragma unroll 1
+      for (int q = 0; q < 2; ++q) team_helper<160, W, WV>(s2, t2, P, park, seq);  // bins 160, 144
       team_helper<128, W, WV>(s1, t1, P, park, seq);
       team_helper<96, W, WV>(s0, t0, P, park, seq);
     } else {

@@ -120,6 +120,9 @@ __device__ __forceinline__ float col4_sum(float v) {
   return a + b;
 }
 
+// sum over the wave, result in every lane
+__device__ __forceinline__ float wave_sum(float v) { return col4_sum(row16_sum(v)); }
+
 // Lane id the compiler cannot see as loop invariant: every phase re-derives its lane-dependent
 // addresses locally instead of the persistent loops hoisting them (and spilling them) for the
 // whole instance.
@@ -136,9 +139,10 @@ __device__ __forceinline__ int opaque_lane() {
 // ------------------------------------------------------------------------------------------
 // diagnostic build only (-DCMPC_STAMPS): per-phase s_memtime cycle totals.  Phases: 0 condense
 // (+tile load), 1 invert, 2 gradient, 3 symv, 4 polish (all of it), 5 instance total,
-// 6 setup, 7 ADMM iteration outside gradient/symv, 14 polish setup, 15 output (+final gradient);
-// counters: 8 condense+invert calls, 9 polish attempts,
-// 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls.
+// 6 setup, 7 ADMM iteration outside gradient/symv, 14 polish setup, 15 output (+final gradient),
+// 28 face downdates (their symvs included); counters: 8 condense+invert calls, 9 polish
+// attempts, 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls, 29 downdated
+// repairs, 30 downdated faces (16-27: team-mode phases, cmpc_team.hip).
 // ------------------------------------------------------------------------------------------
 #ifdef CMPC_STAMPS
 __device__ unsigned long long g_stamps[32];
@@ -245,6 +249,12 @@ constexpr bool kRhoLowHeavy = CMPC_RHO_LOW_HEAVY;
 constexpr bool kRepairHalf = CMPC_REPAIR_HALF;
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
+// Face downdates (round 4, face_downdate): a repair that only adds faces downdates the inverse
+// instead of refactoring (team mode: off)
+#ifndef CMPC_DOWNDATE
+#define CMPC_DOWNDATE 1
+#endif
+constexpr bool kDowndate = CMPC_DOWNDATE;
 constexpr float kLooseTol = 5.f;
 // After its first failed polish session an instance continues ADMM at kFailRho x rho0.  The
 // slow instances are the ones whose repairs cycle between neighbouring face sets (a degenerate
@@ -435,12 +445,55 @@ __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL]
   WSYNC();
 }
 
+// D = L diag(1 / i) L' of a symmetric 4x4 block (row-major Dm, lower part read), unit lower L
+struct Ldl4 {
+  float i0, i1, i2, i3;            // reciprocal pivots
+  float l10, l20, l30, l21, l31, l32;
+};
+__device__ __forceinline__ Ldl4 ldl4(const float (&Dm)[16]) {
+  Ldl4 f;
+  f.i0 = __builtin_amdgcn_rcpf(Dm[0]);
+  f.l10 = Dm[4] * f.i0; f.l20 = Dm[8] * f.i0; f.l30 = Dm[12] * f.i0;
+  f.i1 = __builtin_amdgcn_rcpf(Dm[5] - f.l10 * Dm[4]);
+  const float u21 = Dm[9] - f.l20 * Dm[4], u31 = Dm[13] - f.l30 * Dm[4];
+  f.l21 = u21 * f.i1; f.l31 = u31 * f.i1;
+  f.i2 = __builtin_amdgcn_rcpf(Dm[10] - f.l20 * Dm[8] - f.l21 * u21);
+  const float u32 = Dm[14] - f.l30 * Dm[8] - f.l31 * u21;
+  f.l32 = u32 * f.i2;
+  f.i3 = __builtin_amdgcn_rcpf(Dm[15] - f.l30 * Dm[12] - f.l31 * u31 - f.l32 * u32);
+  return f;
+}
+
+// The rank-4 MFMA operands of Y diag(1 / dl) Y' with Y = P^ L^-T for panel rows ph[I] (row
+// 16 I + c of the 4-column panel): a[I] = -Y[16 I + c][g], b[I] = Y[16 I + c][g] / dl_g
+template <int NC>
+__device__ __forceinline__ void ldl4_operands(const Ldl4& f, const f4 (&ph)[Cfg<NC>::TT], int g,
+                                              float (&a)[Cfg<NC>::TT], float (&b)[Cfg<NC>::TT]) {
+  using C = Cfg<NC>;
+  const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
+  // y_g = (P^ L^-T)_g = sum_m L^-1[g][m] P^_m: this lane's row of L^-1 (unit lower) and
+  // 1/dl_g, selected once per step, so each panel row costs four FMAs and no branches
+  const float n10 = -f.l10, n21 = -f.l21, n32 = -f.l32;
+  const float n20 = f.l21 * f.l10 - f.l20, n31 = f.l32 * f.l21 - f.l31;
+  const float n30 = -f.l30 - f.l31 * n10 - f.l32 * n20;
+  const float w0 = g3 ? n30 : g2 ? n20 : g1 ? n10 : 1.f;
+  const float w1 = g3 ? n31 : g2 ? n21 : g1 ? 1.f : 0.f;
+  const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
+  const float w3 = g3 ? 1.f : 0.f;
+  const float ig = g3 ? f.i3 : g2 ? f.i2 : g1 ? f.i1 : f.i0;
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
+    a[I] = -yg;
+    b[I] = yg * ig;
+  }
+}
+
 // LDL of the 4x4 pivot block (rows k0..k0+3 of the panel) and the step's MFMA operands
 template <int NC, class SM>
 __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
                                                float (&a)[Cfg<NC>::TT], float (&b)[Cfg<NC>::TT]) {
   using C = Cfg<NC>;
-  const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
   float Dm[16];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -451,29 +504,7 @@ __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
   f4 ph[C::TT];
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
-  const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
-  const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
-  const float i1 = __builtin_amdgcn_rcpf(Dm[5] - l10 * Dm[4]);
-  const float u21 = Dm[9] - l20 * Dm[4], u31 = Dm[13] - l30 * Dm[4];
-  const float l21 = u21 * i1, l31 = u31 * i1;
-  const float i2 = __builtin_amdgcn_rcpf(Dm[10] - l20 * Dm[8] - l21 * u21);
-  const float u32 = Dm[14] - l30 * Dm[8] - l31 * u21;
-  const float l32 = u32 * i2;
-  const float i3 = __builtin_amdgcn_rcpf(Dm[15] - l30 * Dm[12] - l31 * u31 - l32 * u32);
-  const float n10 = -l10, n21 = -l21, n32 = -l32;
-  const float n20 = l21 * l10 - l20, n31 = l32 * l21 - l31;
-  const float n30 = -l30 - l31 * n10 - l32 * n20;
-  const float w0 = g3 ? n30 : g2 ? n20 : g1 ? n10 : 1.f;
-  const float w1 = g3 ? n31 : g2 ? n21 : g1 ? 1.f : 0.f;
-  const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
-  const float w3 = g3 ? 1.f : 0.f;
-  const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
-    const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
-    a[I] = -yg;
-    b[I] = yg * ig;
-  }
+  ldl4_operands<NC>(ldl4(Dm), ph, g, a, b);
 }
 
 // rank-4 update of the tiles whose criticality for pivot block Kc is CRIT
@@ -1133,16 +1164,25 @@ __device__ __forceinline__ void build_admm_basis(Smem<NC>& s, const KParams& P,
 }
 
 // Polish setup: the reduced basis of the faces in s.code (lane t owns triple t),
-// u = T v + t0 with t0 = locked components, v initialised from z.  Returns nr; the param
-// indices of each triple are left packed in s.fpk for the KKT check.
+// u = T v + t0 with t0 = locked components, v initialised from the triple forces in `vsrc`
+// (ADMM's z, or the candidate forces a polish check left in s.dl; read before anything is
+// written, since s.dl shares the G slab).  Returns nr; the param indices of each triple are
+// left packed in s.fpk for the KKT check.
 template <int NC>
 __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
-                                            const float* __restrict__ Bg, int ntri) {
+                                            const float* __restrict__ Bg, int ntri,
+                                            const float* vsrc) {
   const int lane = opaque_lane();
   const int N = P.N;
   const float mu = P.mu, fzmin = P.fz_min;
   WSYNC();
   const bool owns = lane < ntri;
+  float vs[3] = {0.f, 0.f, 0.f};
+  if (owns) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) vs[a] = vsrc[3 * lane + a];
+  }
+  WSYNC();
   const int code = owns ? s.code[lane] : 0;
   const int kl = owns ? s.tri[lane] : 0;
   const int k = kl >> 2, leg = kl & 3;
@@ -1172,7 +1212,7 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
       for (int r = 0; r < 12; ++r) s.Bt[px * kBS + r] = bx[r];
       s.Rt[px] = s.R2[3 * leg];
       s.par[px] = k;
-      s.v[px] = s.z[3 * lane];
+      s.v[px] = vs[0];
     }
     if (sy == 0) {
       py = p++;
@@ -1180,7 +1220,7 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
       for (int r = 0; r < 12; ++r) s.Bt[py * kBS + r] = by[r];
       s.Rt[py] = s.R2[3 * leg + 1];
       s.par[py] = k;
-      s.v[py] = s.z[3 * lane + 1];
+      s.v[py] = vs[1];
     }
     if (!zl) {
       pz = p++;
@@ -1190,7 +1230,7 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
       s.Rt[pz] = s.R2[3 * leg + 2] + mu * mu * ((sx != 0 ? s.R2[3 * leg] : 0.f) +
                                                 (sy != 0 ? s.R2[3 * leg + 1] : 0.f));
       s.par[pz] = k;
-      s.v[pz] = s.z[3 * lane + 2];
+      s.v[pz] = vs[2];
     } else {  // fz locked at fz_min: the triple's constant force t0 enters d~ through B_k t0
       const float tx = sx * mu * fzmin, ty = sy * mu * fzmin;
 #pragma unroll
@@ -1234,7 +1274,8 @@ __device__ __forceinline__ int polish_setup(Smem<NC>& s, const KParams& P,
 template <int NC>
 __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
                                              const float* __restrict__ Bg, int ntri, float step,
-                                             bool& changed, bool& loose, int top = 0) {
+                                             bool& changed, bool& loose, bool& converged,
+                                             int top = 0) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
   float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -1249,11 +1290,13 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   const int sy = (code & 8) ? 1 : ((code & 16) ? -1 : 0);
   const bool zl = (code & 1) != 0;
   if (owns) {
+    // the forces from the basis params (a face added by a downdate keeps its param, which the
+    // constraint holds on the face to rounding); the KKT conditions below use the current faces
     const int pk = s.fpk[lane];
     const int px = pk & 255, py = (pk >> 8) & 255, pz = (pk >> 16) & 255;
-    fz = zl ? fzmin : s.v[pz];
-    fx = (sx == 0) ? s.v[px] : sx * mu * fz;
-    fy = (sy == 0) ? s.v[py] : sy * mu * fz;
+    fz = (pz == 255) ? fzmin : s.v[pz];
+    fx = (px == 255) ? sx * mu * fz : s.v[px];
+    fy = (py == 255) ? sy * mu * fz : s.v[py];
     const float* Bk = Bg + k * 144 + 3 * leg;
     float ax = 0.f, ay = 0.f, az = 0.f;
 #pragma unroll
@@ -1317,6 +1360,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   if (owns) s.tcnt[lane] = nc;  // repaired code (copied into s.code by the caller if used)
   changed = __any(owns && nc != code) != 0;
   const bool step_ok = step <= P.polish_tol * us;
+  converged = step_ok;
   loose = (__all(lok) != 0) && step_ok;
   const bool all_ok = (__all(ok) != 0) && step_ok;
   if (all_ok && owns) {
@@ -1325,6 +1369,142 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     s.x[3 * lane + 2] = fz;
   }
   return all_ok;
+}
+
+// ------------------------------------------------------------------------------------------
+// Face downdates (round 4).  A repair that only ADDS faces to the current face set keeps the
+// basis and the inverse M of the last factorization: each added face is an equality a'v = c on
+// the basis params (fz at fz_min: v_pz = fz_min; fx on the face of sign s: v_px - s mu v_pz = 0,
+// or v_px = s mu fz_min where the basis locks fz; fy alike), and the inverse on the constrained
+// set is the sequence of rank-1 downdates
+//     M_j = M_{j-1} - w_j w_j' / d_j,   w_j = M_{j-1} a_j,   d_j = a_j' w_j,
+// kept ASIDE: M stays in the register tiles untouched, the w_j are vectors in the polish
+// session's free LDS (the sweep scaling / panel / H slab), and every refinement step applies
+//     M_F g = M g - sum_j w_j (w_j' g) / d_j
+// after its symv (dd_apply: one wave reduction per face).  w_j is one symv with the sparse a_j
+// (two params at most) minus the earlier faces' terms, whose w_i' a_j are two LDS reads.  v is
+// projected onto each new equality in the M_{j-1} metric, v -= w_j (a_j' v - c_j) / d_j, which
+// keeps the earlier ones (a_i' w_j = 0, i < j).  Cost: a symv per added face instead of a
+// condensation + inversion (~150 k cycles).  (Rank-4 MFMA updates of the tiles themselves do the
+// same arithmetic, but writing the tiles in the polish branch kept them live across the KKT
+// check and the register allocator spilled 600-1,100 VGPRs in every variant tried.)  NumPy model
+// (tests/algo_spec.py downdate=True, the fp32 sweep inverse): unchanged refinement counts, half of
+// all repairs are pure additions, and 6 faces per factorization keep almost all of the gain
+// (config 3: 2.37 -> 2.19 factorizations per instance, the slowest instances -20 %).
+#ifndef CMPC_DD_CAP
+#define CMPC_DD_CAP 6
+#endif
+// faces per factorization: the w_j fill the ds / pan / H slab (5 NC + kMaxP floats) but its
+// last 32 floats, which hold the faces' 1 / d_j, params, coefficients and right-hand sides
+__host__ __device__ constexpr int dd_max(int NC) {
+  return (5 * NC + kMaxP - 32) / NC < CMPC_DD_CAP ? (5 * NC + kMaxP - 32) / NC : CMPC_DD_CAP;
+}
+template <int NC>
+__device__ __forceinline__ float* dd_w(Smem<NC>& s, int j) { return s.ds + j * NC; }
+template <int NC>
+__device__ __forceinline__ float* dd_meta(Smem<NC>& s) { return s.H + kMaxP - 32; }
+
+// Append the faces added by the repair (s.code -> s.tcnt, no drops) as downdates; nadd counts
+// the faces held so far.  False if they do not fit or a d_j is not positive (rounding after
+// many downdates): the caller refactors.
+template <int NC>
+__device__ __forceinline__ bool face_downdate(Smem<NC>& s, const KParams& P,
+                                              const f4 (&M)[Cfg<NC>::NTL], int n, int ntri,
+                                              int& nadd) {
+  static_assert(dd_max(NC) >= 1 && dd_max(NC) <= 8, "the meta block holds 8 faces");
+  static_assert(offsetof(Smem<NC>, H) == offsetof(Smem<NC>, ds) + 5 * NC * sizeof(float),
+                "ds, pan and H are one slab");
+  const int lane = opaque_lane();
+  n = uniform(n);
+  float* meta = dd_meta(s);  // [0, 8) 1 / d_j, [8, 16) p1 | p2 << 8, [16, 24) coefficient, [24, 32) c
+  WSYNC();
+  int F;
+  {
+    const bool owns = lane < ntri;
+    const int oc = owns ? s.code[lane] : 0, nc = owns ? s.tcnt[lane] : 0;
+    const int add = nc & ~oc;
+    const int cnt = (add & 1) + ((add & 6) != 0) + ((add & 24) != 0);
+    int j = nadd + wave_excl_scan4(cnt);
+    F = uniform(wave_total4(cnt));
+    if (nadd + F > dd_max(NC)) return false;  // (uniform)
+    if (owns && add) {
+      // a face with no second param has p2 = p1 and coefficient 0
+      const float mu = P.mu, fzmin = P.fz_min;
+      const int pk = s.fpk[lane];
+      const int px = pk & 255, py = (pk >> 8) & 255, pz = (pk >> 16) & 255;
+      if (add & 1) {  // (first: a friction face added with it then reads fz = fz_min)
+        meta[8 + j] = __int_as_float(pz | (pz << 8)); meta[16 + j] = 0.f; meta[24 + j] = fzmin; ++j;
+      }
+#pragma unroll
+      for (int ax = 0; ax < 2; ++ax) {
+        const int bits = ax ? (add & 24) : (add & 6);
+        if (!bits) continue;
+        const int pa = ax ? py : px;
+        const float sg = (bits & (ax ? 8 : 2)) ? 1.f : -1.f;
+        if (pz != 255) {
+          meta[8 + j] = __int_as_float(pa | (pz << 8)); meta[16 + j] = -sg * mu; meta[24 + j] = 0.f;
+        } else {
+          meta[8 + j] = __int_as_float(pa | (pa << 8)); meta[16 + j] = 0.f; meta[24 + j] = sg * mu * fzmin;
+        }
+        ++j;
+      }
+    }
+  }
+  WSYNC();
+  const int j1 = nadd + F;
+  for (int j = nadd; j < j1; ++j) {  // uniform
+    const int q = __float_as_int(meta[8 + j]);
+    const int p1 = q & 255, p2 = (q >> 8) & 255;
+    const float cf = meta[16 + j], cv = meta[24 + j];
+    for (int p = lane; p < NC; p += 64) s.r[p] = (p == p1) ? 1.f : (p == p2) ? cf : 0.f;
+    float* w = dd_w(s, j);
+    symv<NC>(s, M, n, s.r, w);  // w = M a_j
+    for (int i = 0; i < j; ++i) {  // w -= w_i (w_i' a_j) / d_i  (uniform trip count)
+      const float* wi = dd_w(s, i);
+      const float t = fmaf(cf, wi[p2], wi[p1]) * meta[i];
+      for (int p = lane; p < n; p += 64) w[p] = fmaf(-t, wi[p], w[p]);
+      WSYNC();
+    }
+    const float d = fmaf(cf, w[p2], w[p1]);
+    if (!(d > 0.f) || !isfinite(d)) return false;  // (the same value in every lane)
+    const float id = 1.f / d;
+    const float res = (fmaf(cf, s.v[p2], s.v[p1]) - cv) * id;
+    WSYNC();
+    for (int p = lane; p < n; p += 64) s.v[p] = fmaf(-res, w[p], s.v[p]);  // v onto a_j' v = c_j
+    if (lane == 0) meta[j] = id;
+    WSYNC();
+  }
+  nadd = j1;
+  return true;
+}
+
+// dl = M_F g from dl = M g: dl -= sum_j w_j (w_j' g) / d_j over the nadd faces held
+template <int NC>
+__device__ __forceinline__ void dd_apply(Smem<NC>& s, int n, int nadd, const float* gin,
+                                         float* dl) {
+  const int lane = opaque_lane();
+  const float* meta = dd_meta(s);
+  n = uniform(n);
+  WSYNC();
+  float sj[dd_max(NC)];
+#pragma unroll
+  for (int j = 0; j < dd_max(NC); ++j) {
+    if (j >= nadd) break;  // uniform
+    const float* w = dd_w(s, j);
+    float part = 0.f;
+    for (int p = lane; p < n; p += 64) part = fmaf(w[p], gin[p], part);
+    sj[j] = wave_sum(part) * meta[j];
+  }
+  for (int p = lane; p < n; p += 64) {
+    float acc = dl[p];
+#pragma unroll
+    for (int j = 0; j < dd_max(NC); ++j) {
+      if (j >= nadd) break;
+      acc = fmaf(-sj[j], dd_w(s, j)[p], acc);
+    }
+    dl[p] = acc;
+  }
+  WSYNC();
 }
 
 // park / restore the register-resident inverse in the wave's global slab (uniform base,
@@ -1376,7 +1556,6 @@ constexpr int kIpmIters = 11;
 #endif
 constexpr float kIpmMuStop = CMPC_IPM_MU_STOP;
 
-__device__ __forceinline__ float wave_sum(float v) { return col4_sum(row16_sum(v)); }
 __device__ __forceinline__ float wave_min(float v) { return -wave_max(-v); }
 
 // tiles += G' diag(d) G: the 3x3 block of each triple (d = z / s of its 5 rows at
@@ -1721,7 +1900,7 @@ struct Resume {
   int stage;  // 0: a new instance; 1: the interior-point stage is due; 2: resume after it
   bool ipm_ok, rho_low, seen_start, fail_rho_done;
   float rho, rp, rd, np_, nd;
-  int n, ntri, status, iters, it, nfail, ntried, last_pol, nsfail, nfact;
+  int n, ntri, status, iters, it, nfail, ntried, last_pol, nsfail, nfact, stable;
 #ifdef CMPC_DIAG_COUNTS
   int dg_fact, dg_pol;
   unsigned long long dg_t0;
@@ -1891,6 +2070,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   float shift = uniformf(P.sigma + rho);
   int it = 0;
   int repairs_left = 0;
+  int nadd = 0;           // faces added by downdates since the last factorization
   bool parked = false;    // the ADMM inverse is in the park slab
   int nfail = 0;          // failed sessions so far (the memory holds the last kFailMem)
   int ntried = 0;         // face sets tried in the current session
@@ -1907,7 +2087,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     if (resume) {
       rho = rs->rho; rho_low = rs->rho_low; rp = rs->rp; rd = rs->rd; np_ = rs->np_; nd = rs->nd;
       status = rs->status; iters = rs->iters; it = rs->it; nfail = rs->nfail; ntried = rs->ntried;
-      last_pol = rs->last_pol; nsfail = rs->nsfail; nfact = rs->nfact;
+      last_pol = rs->last_pol; nsfail = rs->nsfail; nfact = rs->nfact; stable = rs->stable;
       seen_start = rs->seen_start; fail_rho_done = rs->fail_rho_done;
 #ifdef CMPC_DIAG_COUNTS
       dg_fact = rs->dg_fact; dg_pol = rs->dg_pol; dg_t0 = rs->dg_t0;
@@ -1925,7 +2105,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
         seen_start = false;
         repairs_left = P.polish_repairs;
-        nact = polish_setup<NC>(s, P, Bg, ntri);
+        nact = polish_setup<NC>(s, P, Bg, ntri, s.z);
         shift = P.sigma;
         in_polish = true;
         last_pol = it;
@@ -1940,7 +2120,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     WSYNC();
     if (lane < ntri) s.code[lane] = s.pcode[lane];
     repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
-    nact = polish_setup<NC>(s, P, Bg, ntri);
+    nact = polish_setup<NC>(s, P, Bg, ntri, s.z);
     shift = P.sigma;
     in_polish = true;
   }
@@ -1975,6 +2155,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         gradient<NC, (W > 1)>(s, P, nact, s.v, s.g, pwc, twc);
         if constexpr (W == 1) {
           symv<NC>(s, M, nact, s.g, s.dl);
+          if constexpr (kDowndate) {
+            if (nadd > 0) dd_apply<NC>(s, nact, nadd, s.g, s.dl);  // (uniform)
+          }
         } else {
           team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
         }
@@ -1999,11 +2182,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // a hard instance's later repairs move only the worst triples: full primal-dual
       // active-set steps swap several faces at a time and can wander between neighbouring sets
       const int top = (kRepairTop > 0 && (nfail > 0 || ntried >= 3)) ? kRepairTop : 0;
-      const bool ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, top);
+      bool converged = false;
+      const bool ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, top);
 #ifdef CMPC_TRACE
       if (b == CMPC_TRACE && lane == 0)
-        printf("it %d polish nact %d ok %d loose %d changed %d step %g repairs_left %d\n", it, nact,
-               (int)ok, (int)loose, (int)changed, step, repairs_left);
+        printf("it %d polish nact %d nadd %d ok %d loose %d changed %d step %g repairs_left %d\n", it,
+               nact, nadd, (int)ok, (int)loose, (int)changed, step, repairs_left);
 #endif
       CMPC_ACC(4, t_pol);
       if (ok) {
@@ -2011,15 +2195,42 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         status = 1;
         break;
       }
+      if (nadd > 0 && !converged) {
+        // the downdated inverse stopped contracting: refactor the current face set, from the
+        // candidate forces (not a repair)
+        nact = polish_setup<NC>(s, P, Bg, ntri, s.dl);
+        nadd = 0;
+        shift = P.sigma;
+        refactor = true;
+        continue;
+      }
       if (repairs_left > 0 && changed && !tried_before<NC>(s, ntri, ntried)) {
         // re-polish on the repaired face set
         --repairs_left;
+        bool dd = false;
+        if constexpr (kDowndate && W == 1) {
+          // only added faces: downdate the inverse in the current basis (no refactorization)
+          const int l = opaque_lane();
+          WSYNC();
+          const int oc = (l < ntri) ? s.code[l] : 0, nc = (l < ntri) ? s.tcnt[l] : 0;
+          const int add = nc & ~oc;
+          const int nf = wave_total4((add & 1) + ((add & 6) != 0) + ((add & 24) != 0));
+          if (__any((nc & oc) != oc) == 0 && nadd + nf <= dd_max(NC)) {  // (uniform)
+            CMPC_T0(t_dd);
+            dd = face_downdate<NC>(s, P, M, nact, ntri, nadd);
+            CMPC_ACC(28, t_dd);
+            CMPC_CNT(29, 1);
+            CMPC_CNT(30, nf);
+          }
+        }
         if (lane < ntri) {
           s.code[lane] = s.tcnt[lane];
           if (ntried < kTryMem) s.tpat[ntried][lane] = (uint8_t)s.tcnt[lane];
         }
         if (ntried < kTryMem) ++ntried;
-        nact = polish_setup<NC>(s, P, Bg, ntri);
+        if (dd) continue;  // refine on the downdated inverse
+        nact = polish_setup<NC>(s, P, Bg, ntri, s.z);
+        nadd = 0;
         shift = P.sigma;
         refactor = true;
         continue;
@@ -2076,6 +2287,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           rs->rho = rho; rs->rho_low = rho_low; rs->rp = rp; rs->rd = rd; rs->np_ = np_; rs->nd = nd;
           rs->status = status; rs->iters = iters; rs->it = it; rs->nfail = nfail;
           rs->ntried = ntried; rs->last_pol = last_pol; rs->nsfail = nsfail; rs->nfact = nfact;
+          rs->stable = stable;  // (the back-off set when the failed session started)
           rs->seen_start = seen_start; rs->fail_rho_done = fail_rho_done;
 #ifdef CMPC_DIAG_COUNTS
           rs->dg_fact = dg_fact; rs->dg_pol = dg_pol; rs->dg_t0 = dg_t0;
@@ -2224,7 +2436,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       parked = false;      // a failed polish refactors the ADMM matrix instead
 #endif
       repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
-      nact = polish_setup<NC>(s, P, Bg, ntri);
+      nact = polish_setup<NC>(s, P, Bg, ntri, s.z);
+      nadd = 0;
       CMPC_ACC(14, t_ps);
       shift = P.sigma;
       refactor = true;
@@ -2391,23 +2604,34 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
 #endif
 constexpr size_t kLdsSlot = CMPC_LDS_SLOT;
 
+// LDS image of a group kernel's bins (NCB = 0: a single-bin kernel)
+template <int NC>
+constexpr size_t smem_size() {
+  if constexpr (NC == 0) return 0;
+  else return sizeof(Smem<NC>);
+}
+
 // One persistent kernel per register class: bins NCA and NCB share the occupancy (two waves per
-// SIMD for NC <= 128, one for NC >= 160), so one kernel serves both, draining the larger bin
-// first (its instances are the slower ones: hardest first shortens the batch tail).  Two
-// kernels instead of four keep the solve within the device's hardware queues (the caller's
-// stream + one plan stream), so the two classes really overlap.  IPM: the variant with the
-// interior-point fallback for hard instances (used for tail-bound batches).
+// SIMD for NC <= 128, one for NC >= 144), so one kernel serves both, draining the larger bin
+// first (its instances are the slower ones: hardest first shortens the batch tail).  NCB = 0:
+// one bin (the NC = 192 kernel).  Kernels submitted concurrently on their own streams (the
+// caller's + two plan streams) stay within the device's hardware queues, so the classes really
+// overlap.  IPM: the variant with the interior-point fallback for hard instances (variant
+// builds only, -DCMPC_WITH_IPM).
 template <int NCA, int NCB, bool IPM>
 __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
     solve_group_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ list_a,
                        const int* __restrict__ list_b, const int* __restrict__ counts,
                        int* __restrict__ heads, int qa, float* __restrict__ work,
                        size_t slab) {
-  static_assert(Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
-  constexpr size_t kImg = sizeof(Smem<NCA>) > sizeof(Smem<NCB>) ? sizeof(Smem<NCA>)
-                                                                 : sizeof(Smem<NCB>);
+  static_assert(NCB == 0 || Cfg<NCA>::WPE == Cfg<NCB>::WPE, "a group shares one occupancy class");
+  constexpr size_t kImg = smem_size<NCA>() > smem_size<NCB>() ? smem_size<NCA>() : smem_size<NCB>();
   constexpr size_t kBytes = kLdsSlot ? (kImg + kLdsSlot - 1) / kLdsSlot * kLdsSlot : kImg;
   static_assert(!kLdsSlot || 4 * kBytes <= 160 * 1024, "one wave per SIMD must fit the CU's LDS");
+  // the two-wave class must stay within ONE slot: a layout change that rounds it up to two
+  // would halve its waves per CU (and break the heavy-first hand-over of freed LDS)
+  static_assert(!kLdsSlot || Cfg<NCA>::WPE == 1 || kImg <= kLdsSlot, "NC <= 128 image exceeds the LDS slot");
+  static_assert(Cfg<NCA>::WPE * 4 * kBytes <= 160 * 1024, "the class's waves per CU must fit the LDS");
   __shared__ __attribute__((aligned(16))) unsigned char raw[kBytes];
   float* park = work + (size_t)blockIdx.x * slab;
 #ifdef CMPC_STAMPS
@@ -2417,15 +2641,17 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
 #endif
   drain_bin<NCA, 1, IPM>(*reinterpret_cast<Smem<NCA>*>(raw), P, in, out, list_a, counts + qa,
                          heads + qa, park);
-  drain_bin<NCB, 1, IPM>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b, counts + qa - 1,
-                         heads + qa - 1, park);
+  if constexpr (NCB > 0) {
+    drain_bin<NCB, 1, IPM>(*reinterpret_cast<Smem<NCB>*>(raw), P, in, out, list_b,
+                           counts + qa - 1, heads + qa - 1, park);
+  }
 #ifdef CMPC_STAMPS
   WSYNC();
   if (threadIdx.x < 32) atomicAdd(&g_stamps[threadIdx.x], s0.st[threadIdx.x]);
 #endif
 }
 
-// Team mode (cmpc_team.hip): one workgroup of W waves per QP, one kernel for all four bins
+// Team mode (cmpc_team.hip): one workgroup of W waves per QP, one kernel for all five bins
 // (heaviest first: the slow instances start first).  Wave 0 leads (drain loop +
 // solve_instance), waves 1..W-1 serve its matrix commands; at most two workgroups per CU
 // (<= 256 VGPRs per wave: the tiles are split W ways, so every bin fits the same class and a
@@ -2459,8 +2685,12 @@ __global__ void __launch_bounds__(64 * W, 2)
   if (threadIdx.x < 32) s1.st[threadIdx.x] = 0;
 #endif
   if (w == 0) {
-    drain_bin<192, W>(s3, P, in, out, lists + 3 * stride, counts + 3, heads + 3, park, &t3, &seq);
-    drain_bin<160, W>(s2, P, in, out, lists + 2 * stride, counts + 2, heads + 2, park, &t2, &seq);
+    drain_bin<192, W>(s3, P, in, out, lists + 4 * stride, counts + 4, heads + 4, park, &t3, &seq);
+    // bins 3 (NC 160) and 2 (NC 144) in the NC = 160 image (team mode pairs tile columns, so
+    // TT must be even); one copy of the code
+#pragma unroll 1
+    for (int q = 3; q >= 2; --q)
+      drain_bin<160, W>(s2, P, in, out, lists + q * stride, counts + q, heads + q, park, &t2, &seq);
     drain_bin<128, W>(s1, P, in, out, lists + stride, counts + 1, heads + 1, park, &t1, &seq);
     drain_bin<96, W>(s0, P, in, out, lists, counts, heads, park, &t0, &seq);
   } else {

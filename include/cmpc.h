@@ -47,7 +47,8 @@
 extern "C" {
 #endif
 
-#define CMPC_ABI_VERSION 3
+/* 4: three solve-kernel timing slots (CMPC_NUM_SOLVE_KERNELS); cmpc_params is unchanged from 3 */
+#define CMPC_ABI_VERSION 4
 
 #define CMPC_OK 0
 #define CMPC_E_INVALID (-22)   /* bad argument / parameter (EINVAL) */
@@ -77,12 +78,14 @@ typedef struct cmpc_params {
   float polish_tol;       /* relative KKT tolerance for accepting the polished point */
   int32_t polish_repairs; /* active-set repairs (add violated / drop negative-multiplier faces
                              and re-polish) before resuming ADMM */
-  int32_t ipm_facts;      /* an instance that has failed a polish session and spent this many
-                             factorizations identifies its face set by interior-point steps
-                             (hard instances); 0 = never.  Default 0: with the
-                             damped repairs the variants without the fallback are faster on
-                             every measured batch (config 3 at 8,192 2.86 -> 2.25 ms); 8 was
-                             the default before them */
+  int32_t ipm_facts;      /* EXPERIMENTAL, variant builds only (-DCMPC_WITH_IPM): an instance that
+                             has failed a polish session and spent this many factorizations
+                             identifies its face set by interior-point steps (hard instances,
+                             DESIGN.md 4h); 0 = never.  Default 0: with the damped repairs the
+                             variants without the fallback are faster on every measured batch
+                             (config 3 at 8,192 2.86 -> 2.25 ms).  The default library does
+                             not carry those kernels: cmpc_plan_create rejects ipm_facts > 0
+                             (CMPC_E_INVALID) there */
   int32_t check_termination; /* ADMM iterations between termination tests (OPTS check_termination,
                              centroidal_mpc.py:31): the polish trigger (face set stable for
                              polish_stable iterations -> active-set polish + KKT check, the only
@@ -243,19 +246,22 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
 
 /* Measurement hooks (not on the reference's interface; used by bench.py).  A solve launches at
  * most CMPC_NUM_SOLVE_KERNELS persistent solve kernels; cmpc_plan_solve_kernel names solve
- * kernel k (0 or 1) of a batch of B instances, or returns NULL if that slot is not launched:
+ * kernel k (0, 1 or 2) of a batch of B instances, or returns NULL if that slot is not launched:
  *   B <= cmpc_plan_team_batch:  "solve_team_kernel<4>" (k = 0 only);
  *   larger batches:             "solve_group_kernel<128, 96, IPM>" (k = 0, the NC <= 128
- *                               class) and "solve_group_kernel<192, 160, IPM>" (k = 1, the
- *                               NC >= 160 class; NULL if N is too short to need it); IPM = true
- *                               for B <= cmpc_plan_ipm_batch.  Slots are per class, whichever
- *                               of the two is submitted first (cmpc_plan_set_heavy_first).
+ *                               class), "solve_group_kernel<160, 144, IPM>" (k = 1, the
+ *                               NC 144 / 160 class; NULL if N is too short to need it) and
+ *                               "solve_group_kernel<192, 0, IPM>" (k = 2, the NC 192 bin, more
+ *                               than 160 free forces; NULL if N is too short); IPM = true for
+ *                               B <= cmpc_plan_ipm_batch in -DCMPC_WITH_IPM builds.  Slots are
+ *                               per kernel, whichever class is submitted first
+ *                               (cmpc_plan_set_heavy_first).
  * While enabled, cmpc_solve records a hipEvent pair around each solve-kernel launch on the
  * stream it is launched on; cmpc_plan_timing_read waits for the recorded events, returns the
  * summed milliseconds per kernel slot (ms_per_kernel[CMPC_NUM_SOLVE_KERNELS]) and the launch
  * counts since the last read, and resets them.  At most 4096 x CMPC_NUM_SOLVE_KERNELS launches
  * are recorded between reads (later ones are not timed). */
-#define CMPC_NUM_SOLVE_KERNELS 2
+#define CMPC_NUM_SOLVE_KERNELS 3
 int cmpc_plan_set_timing(cmpc_plan* plan, int enable);
 int cmpc_plan_timing_read(cmpc_plan* plan, float* ms_per_kernel, int32_t* calls_per_kernel);
 const char* cmpc_plan_solve_kernel(const cmpc_plan* plan, int64_t B, int k);
@@ -263,13 +269,13 @@ const char* cmpc_plan_solve_kernel(const cmpc_plan* plan, int64_t B, int k);
 /* Small-batch mode.  A solve of B <= max_batch instances runs each QP on a workgroup of four
  * waves (one per SIMD of a CU) that split the condensation, the inversion and the matrix-vector
  * products, instead of one wave per QP: B = 256 on 256 CUs otherwise leaves 3 of every 4 SIMDs
- * idle.  All four bins then run in one kernel on `stream` (timed as solve kernel 0).  Results
+ * idle.  All five bins then run in one kernel on `stream` (timed as solve kernel 0).  Results
  * are the same algorithm's (parity-tested in both modes).  max_batch = -1 (the default) selects
  * it for B <= 4 x CUs; 0 disables it.  cmpc_plan_team_batch returns the effective bound. */
 int cmpc_plan_set_team(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
 
-/* Tail-bound batches.  When cmpc_params.ipm_facts > 0 (opt-in), a batch of B <= max_batch
+/* Tail-bound batches (variant builds with -DCMPC_WITH_IPM).  When cmpc_params.ipm_facts > 0, a batch of B <= max_batch
  * instances (one wave per QP, i.e. above the small-batch bound) runs the kernel variants that
  * carry the interior-point fallback for hard instances: a small batch or an N-GPU
  * shard takes as long as its slowest instance.  Large batches run the variants without it (its
@@ -279,10 +285,11 @@ int cmpc_plan_set_ipm(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_ipm_batch(const cmpc_plan* plan, int64_t* max_batch);
 
 /* Launch order of the two register classes.  A batch above the small-batch bound launches one
- * persistent kernel per register class (NC <= 128: two waves per SIMD; NC >= 160: one); the
+ * persistent kernel per register class (NC <= 128: two waves per SIMD; NC 144 / 160: one; plus
+ * the NC 192 bin's kernel, submitted before both on its own stream); the
  * class submitted first fills the device and the other takes SIMDs as they free up, so the
  * step ends with the tail of the class that runs second.  Batches of B >= min_batch submit the
- * NC >= 160 class first (its tail is then filled by NC <= 128 waves: config 3 at 65,536 and
+ * NC 144 / 160 class first (its tail is then filled by NC <= 128 waves: config 3 at 65,536 and
  * 16,384 faster), smaller ones the NC <= 128 class (config 2 at 4,096 faster).  Results do not
  * depend on the order (each instance is solved by one wave, deterministically).
  * min_batch = -1 (the default) selects B > 16 x CUs; 0 never.  cmpc_plan_heavy_first_batch

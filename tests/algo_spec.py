@@ -16,7 +16,8 @@ class Params:
                  alpha=1.6, max_iter=400, stable_checks=3, adaptive_interval=25,
                  eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=6,
                  fail_rho=4.0, late_repairs=3, backoff_cap=3, repair_top=2,
-                 repair_top_from=1, repair_top_rep=2, repair_frac=0.5, stable_grow=3):
+                 repair_top_from=1, repair_top_rep=2, repair_frac=0.5, stable_grow=3,
+                 fp32_polish=False, downdate=False, dd_max=24, hook=None):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -33,6 +34,10 @@ class Params:
         self.repair_top_rep = repair_top_rep    # ... or from this repair of any session on
         self.repair_frac = repair_frac          # ... at least this fraction of the changed triples
         self.stable_grow = stable_grow          # required face-set stability x this per failed session
+        self.fp32_polish = fp32_polish          # polish preconditioner: the kernel's fp32 sweep inverse
+        self.downdate = downdate                # face-adding repairs as downdates of the inverse
+        self.dd_max = dd_max                    # ... up to this many added faces per factorization
+        self.hook = hook                        # (studies) dict filled at the first polish session
 
 
 def project(v, mu, fz_min):
@@ -93,6 +98,23 @@ def condense(A, Bt, Q, Rt, shift):
     return H
 
 
+def sweep_inverse32(H):
+    """The kernel's polish inverse in fp32: unit-diagonal scaling, then the symmetric sweep
+    (Gauss-Jordan) pivot by pivot in fp32 (the 4-pivot block form keeps the scalar sweep's
+    accuracy); M holds -(scaled inverse) until the sign and scaling are undone."""
+    H = np.asarray(H, np.float64)
+    n = H.shape[0]
+    dsc = (1.0 / np.sqrt(np.diag(H))).astype(F32)
+    T = (H.astype(F32) * dsc[:, None] * dsc[None, :]).astype(F32)
+    for k in range(n):
+        piv = T[k, k]
+        col = T[:, k].copy()
+        col[k] = piv - F32(1)
+        T = (T - np.outer(col, col / piv)).astype(F32)
+        T[k, k] -= F32(2)
+    return (-T * dsc[:, None] * dsc[None, :]).astype(F32)
+
+
 def solve(inst, p: Params):
     """Solve one instance. inst: dict with Ad, Bd, gd, x0, xref (N,12), contact (4,N)."""
     N = p.N
@@ -106,7 +128,11 @@ def solve(inst, p: Params):
     nf = len(free)
     fidx = np.array([12 * k + 3 * l + a for (k, l, a) in free])
 
+    stats = dict(fact=0, refine=0, dd_faces=0, dd_batches=0, dd_fallback=0, sessions=0,
+                 repairs=0, dd_repairs=0)
+
     def admm_matrix(rho):
+        stats['fact'] += 1
         Bt = [B[k][:, [3 * l + a for l in range(4) if stance[k, l] for a in range(3)]] for k in range(N)]
         Rt = np.concatenate([np.tile(p.R[[3 * l + a for a in range(3)]], 1) for k in range(N) for l in range(4) if stance[k, l]]) if nf else np.zeros(0, F32)
         H = condense(A, Bt, p.Q, Rt, p.sigma + rho)
@@ -119,26 +145,34 @@ def solve(inst, p: Params):
     def full(v):
         u = np.zeros(12 * N, F32); u[fidx] = v; return u.reshape(N, 12)
 
-    def polish(zv, code):
-        # faces per stance triple
+    tri = [(k, l) for k in range(N) for l in range(4) if stance[k, l]]
+
+    def make_basis(code):
+        """Reduced basis of the faces in `code` (cmpc_wave.hip polish_setup) and its factorization:
+        u = T v + t0; pidx[t] = (px, py, pz) of triple t (-1: no param)."""
+        stats['fact'] += 1
         Bt = []; Rt = []; params = []
         t0 = np.zeros(12 * N, F32)
+        pidx = np.full((len(tri), 3), -1, int)
         ti = 0
         for k in range(N):
             cols = []
             for l in range(4):
                 if not stance[k, l]:
                     continue
-                c = code[ti]; ti += 1
+                c = code[ti]
                 sx = 1 if c & 2 else (-1 if c & 4 else 0)
                 sy = 1 if c & 8 else (-1 if c & 16 else 0)
                 zl = bool(c & 1)
                 base = 3 * l
                 if sx == 0:
+                    pidx[ti, 0] = len(params)
                     cols.append(B[k][:, base]); Rt.append(p.R[base]); params.append((k, l, 'x', sx, sy))
                 if sy == 0:
+                    pidx[ti, 1] = len(params)
                     cols.append(B[k][:, base + 1]); Rt.append(p.R[base + 1]); params.append((k, l, 'y', sx, sy))
                 if not zl:
+                    pidx[ti, 2] = len(params)
                     col = B[k][:, base + 2] + sx * p.mu * B[k][:, base] + sy * p.mu * B[k][:, base + 1]
                     cols.append(col)
                     Rt.append(p.R[base + 2] + p.mu * p.mu * ((sx != 0) * p.R[base] + (sy != 0) * p.R[base + 1]))
@@ -147,94 +181,187 @@ def solve(inst, p: Params):
                     t0[12 * k + base + 2] = p.fz_min
                     t0[12 * k + base] = sx * p.mu * p.fz_min
                     t0[12 * k + base + 1] = sy * p.mu * p.fz_min
+                ti += 1
             Bt.append(np.stack(cols, 1).astype(F32) if cols else np.zeros((12, 0), F32))
-        nr = len(params)
         H = condense(A, Bt, p.Q, np.array(Rt, F32), p.sigma)
-        L = np.linalg.cholesky(H.astype(np.float64)).astype(F32)
-        zf = full(zv).reshape(-1)
+        bs = dict(params=params, t0=t0, pidx=pidx, code=np.array(code).copy(), nr=len(params))
+        if p.fp32_polish or p.downdate:
+            # an explicit inverse: fp32 as the kernel's sweep computes it, or float64
+            bs['M'] = sweep_inverse32(H) if p.fp32_polish else np.linalg.inv(H.astype(np.float64))
+        else:
+            bs['L'] = np.linalg.cholesky(H.astype(np.float64)).astype(F32)
+        return bs
 
-        def expand(v):
-            u = t0.copy()
-            for (val, (k, l, ax, sx, sy)) in zip(v, params):
-                b = 12 * k + 3 * l
-                if ax == 'x': u[b] = val
-                elif ax == 'y': u[b + 1] = val
-                else:
-                    u[b + 2] = val; u[b] += sx * p.mu * val; u[b + 1] += sy * p.mu * val
-            return u
+    def apply_inv(bs, r):
+        if 'M' in bs:
+            return (bs['M'] @ r.astype(bs['M'].dtype)).astype(F32)
+        return solve_L(bs['L'], r)
 
-        def reduce(g):
-            out = np.zeros(nr, F32)
-            for i, (k, l, ax, sx, sy) in enumerate(params):
-                b = 12 * k + 3 * l
-                if ax == 'x': out[i] = g[b]
-                elif ax == 'y': out[i] = g[b + 1]
-                else: out[i] = g[b + 2] + sx * p.mu * g[b] + sy * p.mu * g[b + 1]
-            return out
+    def expand(bs, v):
+        u = bs['t0'].copy()
+        for (val, (k, l, ax, sx, sy)) in zip(v, bs['params']):
+            b = 12 * k + 3 * l
+            if ax == 'x': u[b] = val
+            elif ax == 'y': u[b + 1] = val
+            else:
+                u[b + 2] = val; u[b] += sx * p.mu * val; u[b + 1] += sy * p.mu * val
+        return u
 
-        v = np.array([zf[12 * k + 3 * l + {'x': 0, 'y': 1, 'z': 2}[ax]] for (k, l, ax, sx, sy) in params], F32)
+    def reduce(bs, g):
+        out = np.zeros(bs['nr'], F32)
+        for i, (k, l, ax, sx, sy) in enumerate(bs['params']):
+            b = 12 * k + 3 * l
+            if ax == 'x': out[i] = g[b]
+            elif ax == 'y': out[i] = g[b + 1]
+            else: out[i] = g[b + 2] + sx * p.mu * g[b] + sy * p.mu * g[b + 1]
+        return out
+
+    def v_from(bs, uf):
+        return np.array([uf[12 * k + 3 * l + {'x': 0, 'y': 1, 'z': 2}[ax]]
+                         for (k, l, ax, sx, sy) in bs['params']], F32)
+
+    def refine(bs, v):
         step = np.inf; prev = np.inf
         for q in range(p.polish_refine + 4):   # cmpc_wave.hip kRefineExtra, kRefineRate
-            u = expand(v)
+            stats['refine'] += 1
+            u = expand(bs, v)
             g, _ = gradient(A, B, d, p.Q, p.R, u.reshape(N, 12))
-            dv = solve_L(L, reduce(g.reshape(-1)))
+            dv = apply_inv(bs, reduce(bs, g.reshape(-1)))
             v = v - dv
             step = np.max(np.abs(dv), initial=0)
             if q + 1 >= p.polish_refine and (step <= p.tol_polish * max(1.0, np.max(np.abs(v), initial=0))
                                              or step > 0.5 * prev):
                 break
             prev = step
-        u = expand(v)
+        return v, step
+
+    def check(bs, v, code, step):
+        """KKT check of the faces in `code` at v (forces from the basis, cmpc_wave.hip
+        polish_check); returns ok, u, the repaired code, loose."""
+        u = expand(bs, v)
         g, _ = gradient(A, B, d, p.Q, p.R, u.reshape(N, 12))
         g = g.reshape(-1)
         gs = F32(max(np.max(np.abs(g[fidx])), 1e-30))
         us = F32(max(np.max(np.abs(u)), 1.0))
         ok = bool(step <= p.tol_polish * us)
-        newcode = code.copy()
+        newcode = np.array(code).copy()
         viol = np.full(len(code), -1.0)
-        ti = 0
-        for k in range(N):
-            for l in range(4):
-                if not stance[k, l]:
-                    continue
-                c = code[ti]
-                b = 12 * k + 3 * l
-                sx = 1 if c & 2 else (-1 if c & 4 else 0)
-                sy = 1 if c & 8 else (-1 if c & 16 else 0)
-                fx, fy, fz = u[b:b + 3]
-                lx = -sx * g[b] if sx else 0.0
-                ly = -sy * g[b + 1] if sy else 0.0
-                l0 = g[b + 2] - p.mu * (lx + ly)
-                tol_d = p.tol_polish * gs
-                tol_p = p.tol_polish * us
-                nc = c
-                if sx and lx < -tol_d: ok = False; nc &= ~6
-                if sy and ly < -tol_d: ok = False; nc &= ~24
-                if (c & 1) and l0 < -tol_d: ok = False; nc &= ~1
-                if not sx and abs(fx) > p.mu * fz + tol_p: ok = False; nc |= (2 if fx > 0 else 4)
-                if not sy and abs(fy) > p.mu * fz + tol_p: ok = False; nc |= (8 if fy > 0 else 16)
-                if not (c & 1) and fz < p.fz_min - tol_p: ok = False; nc |= 1
-                newcode[ti] = nc
-                # largest relative violation (cmpc_wave.hip polish_check `viol`)
-                v = max(-lx / gs if sx else 0.0, -ly / gs if sy else 0.0,
-                        -l0 / gs if c & 1 else 0.0,
-                        0.0 if sx else (abs(fx) - p.mu * fz) / us,
-                        0.0 if sy else (abs(fy) - p.mu * fz) / us,
-                        0.0 if c & 1 else (p.fz_min - fz) / us)
-                viol[ti] = v
-                ti += 1
+        for ti, (k, l) in enumerate(tri):
+            c = code[ti]
+            b = 12 * k + 3 * l
+            sx = 1 if c & 2 else (-1 if c & 4 else 0)
+            sy = 1 if c & 8 else (-1 if c & 16 else 0)
+            fx, fy, fz = u[b:b + 3]
+            lx = -sx * g[b] if sx else 0.0
+            ly = -sy * g[b + 1] if sy else 0.0
+            l0 = g[b + 2] - p.mu * (lx + ly)
+            tol_d = p.tol_polish * gs
+            tol_p = p.tol_polish * us
+            nc = c
+            if sx and lx < -tol_d: ok = False; nc &= ~6
+            if sy and ly < -tol_d: ok = False; nc &= ~24
+            if (c & 1) and l0 < -tol_d: ok = False; nc &= ~1
+            if not sx and abs(fx) > p.mu * fz + tol_p: ok = False; nc |= (2 if fx > 0 else 4)
+            if not sy and abs(fy) > p.mu * fz + tol_p: ok = False; nc |= (8 if fy > 0 else 16)
+            if not (c & 1) and fz < p.fz_min - tol_p: ok = False; nc |= 1
+            newcode[ti] = nc
+            # largest relative violation (cmpc_wave.hip polish_check `viol`)
+            vv = max(-lx / gs if sx else 0.0, -ly / gs if sy else 0.0,
+                     -l0 / gs if c & 1 else 0.0,
+                     0.0 if sx else (abs(fx) - p.mu * fz) / us,
+                     0.0 if sy else (abs(fy) - p.mu * fz) / us,
+                     0.0 if c & 1 else (p.fz_min - fz) / us)
+            viol[ti] = vv
         if p.repair_top > 0 and (len(failed_starts) >= p.repair_top_from or cur_rep[0] >= p.repair_top_rep):
             ncand = int(np.sum(newcode != code))
             kk = max(p.repair_top, int(np.ceil(p.repair_frac * ncand)))
             keep = np.argsort(-viol)[kk:]
-            newcode[keep] = code[keep]
-        self_newcode[0] = newcode
-        self_loose[0] = bool(step <= p.tol_polish * us) and bool(np.all(viol <= 5.0 * p.tol_polish))
-        return ok, u
+            newcode[keep] = np.array(code)[keep]
+        loose = bool(step <= p.tol_polish * us) and bool(np.all(viol <= 5.0 * p.tol_polish))
+        return ok, u, newcode, loose
 
-    self_newcode = [None]
+    def face_constraints(bs, code_old, code_new):
+        """Face additions (code_old -> code_new, no drops) as equalities a'v = c on the basis
+        params (cmpc_wave.hip face downdates)."""
+        cons = []
+        for ti, (k, l) in enumerate(tri):
+            add = int(code_new[ti]) & ~int(code_old[ti])
+            if not add:
+                continue
+            px, py, pz = bs['pidx'][ti]
+            # fz lock first: a friction face added with it then reads its fz as fz_min
+            if add & 1:
+                cons.append(({pz: 1.0}, p.fz_min))
+            for bit_p, bit_m, pa in ((2, 4, px), (8, 16, py)):
+                if add & (bit_p | bit_m):
+                    s = 1.0 if add & bit_p else -1.0
+                    if pz >= 0:
+                        cons.append(({pa: 1.0, pz: -s * float(p.mu)}, 0.0))
+                    else:
+                        cons.append(({pa: 1.0}, s * float(p.mu) * float(p.fz_min)))
+        return cons
+
+    def downdate(bs, v, cons):
+        """M <- M - W (A'W)^-1 W' with W = M A, four faces at a time (one panel of the kernel),
+        and v projected onto the new equalities in the M metric."""
+        M = bs['M']
+        for i0 in range(0, len(cons), 4):
+            blk = cons[i0:i0 + 4]
+            Am = np.zeros((bs['nr'], len(blk)), M.dtype)
+            cv = np.zeros(len(blk), M.dtype)
+            for j, (a, c) in enumerate(blk):
+                for idx, val in a.items():
+                    Am[idx, j] = val
+                cv[j] = c
+            W = (M @ Am).astype(M.dtype)
+            S = (Am.T @ W).astype(M.dtype)
+            r = (Am.T @ v.astype(M.dtype) - cv).astype(M.dtype)
+            v = (v - W @ np.linalg.solve(S.astype(np.float64), r.astype(np.float64)).astype(M.dtype)).astype(F32)
+            M = (M - (W @ np.linalg.solve(S.astype(np.float64), W.T.astype(np.float64))).astype(M.dtype)).astype(M.dtype)
+            stats['dd_batches'] += 1
+        stats['dd_faces'] += len(cons)
+        bs = dict(bs); bs['M'] = M
+        bs['nadd'] = bs.get('nadd', 0) + len(cons)
+        return bs, v
+
+    def session(zv, code, budget, tried):
+        """One polish session from ADMM's face set `code`; returns ok, u, the last repaired code
+        and the loose flag."""
+        if p.hook is not None and 'code' not in p.hook:
+            p.hook.update(code=np.array(code).copy(), rho=rho, z=zv.copy())
+        bs = make_basis(code)
+        v = v_from(bs, full(zv).reshape(-1))
+        rep = 0
+        cur_rep[0] = 0
+        while True:
+            v, step = refine(bs, v)
+            ok, u, nc, loose = check(bs, v, code, step)
+            if (not ok and bs.get('nadd', 0) > 0 and
+                    not step <= p.tol_polish * max(1.0, float(np.max(np.abs(u))))):
+                # the downdated preconditioner no longer contracts: refactor the current face set
+                stats['dd_fallback'] += 1
+                bs = make_basis(code)
+                v = v_from(bs, u)
+                continue
+            if ok:
+                return True, u, nc, loose
+            if rep >= budget or np.array_equal(nc, code) or nc.tobytes() in tried[:8]:
+                return False, u, nc, loose
+            tried.append(nc.tobytes())
+            rep += 1
+            cur_rep[0] = rep
+            stats['repairs'] += 1
+            drops = np.any((nc & np.array(code)) != np.array(code))
+            cons = [] if drops or not p.downdate else face_constraints(bs, code, nc)
+            if p.downdate and not drops and bs.get('nadd', 0) + len(cons) <= p.dd_max:
+                stats['dd_repairs'] += 1
+                bs, v = downdate(bs, v, cons)
+            else:
+                bs = make_basis(nc)
+                v = v_from(bs, full(zv).reshape(-1))
+            code = nc
+
     cur_rep = [0]  # repairs made so far in the current session (repair_top_rep)
-    self_loose = [False]
 
     failed_starts = []
     # the NC >= 128 bins (nf > 96) start from rho / 2 and return to rho after their first
@@ -273,21 +400,13 @@ def solve(inst, p: Params):
             start = code.tobytes()
             seen = start in failed_starts[-4:]
             tried = [start]
-            cur_rep[0] = 0
-            ok, u = polish(z, code)
-            rep = 0
+            stats['sessions'] += 1
+            # the ADMM inverse is parked only where a failure restores it (cmpc_wave.hip)
+            parked = not rho_low and len(failed_starts) > 0
             budget = 0 if seen else (min(p.repairs, p.late_repairs) if len(failed_starts) >= 2 else p.repairs)
-            while not ok and rep < budget:   # cmpc_wave.hip kLateRepairs
-                c2 = self_newcode[0]
-                if np.array_equal(c2, code) or c2.tobytes() in tried[:8]:
-                    break
-                code = c2
-                tried.append(code.tobytes())
-                rep += 1
-                cur_rep[0] = rep
-                ok, u = polish(z, code)
+            ok, u, _, loose = session(z, code, budget, tried)
             stable = -backoff  # back off before the next attempt
-            if not ok and self_loose[0]:
+            if not ok and loose:
                 ok = True  # the session ends within the loose tolerance (kLooseTol): accepted
             if ok:
                 status = 1; U = u; break
@@ -298,6 +417,8 @@ def solve(inst, p: Params):
                 rho_low = False; rho = p.fail_rho * p.rho; L = admm_matrix(rho)
             elif rho_low:
                 rho_low = False; rho = p.rho; L = admm_matrix(rho)
+            elif not parked:
+                stats['fact'] += 1  # the polish inverse replaced the ADMM one: refactor
         if p.adaptive_interval and it % p.adaptive_interval == 0:
             rp = np.max(np.abs(x - z)); rd = np.max(np.abs(g + y))
             npn = max(np.max(np.abs(x)), np.max(np.abs(z)), 1e-30)
@@ -309,4 +430,4 @@ def solve(inst, p: Params):
                 rho = nr; L = admm_matrix(rho); rho_low = False
     if U is None:
         U = full(z).reshape(-1)
-    return dict(U=U.reshape(N, 12), status=status, iters=it, nf=nf)
+    return dict(U=U.reshape(N, 12), status=status, iters=it, nf=nf, **stats)

@@ -30,24 +30,36 @@ class _StubPlan:
         return list(self.names)
 
 
-def _batch(n_light, n_heavy, N=16):
+def _batch(n_light, n_heavy, N=16, n_mid=0):
     import numpy as np
-    c = np.zeros((n_light + n_heavy, 4, N), np.uint8)
+    c = np.zeros((n_light + n_mid + n_heavy, 4, N), np.uint8)
     c[:n_light, :, :10] = 1          # 40 stance legs: 120 free forces (NC 128 bin)
-    c[n_light:] = 1                  # 64 stance legs: 192 free forces (NC 192 bin)
-    return c, np.full(n_light + n_heavy, 8, np.int32)
+    c[n_light:n_light + n_mid, :, :13] = 1  # 52 stance legs: 156 free forces (NC 160 bin)
+    c[n_light + n_mid:] = 1          # 64 stance legs: 192 free forces (NC 192 bin)
+    return c, np.full(n_light + n_mid + n_heavy, 8, np.int32)
+
+
+def test_bins_and_kernels():
+    """Five bins (NC 96 / 128 / 144 / 160 / 192) map onto the three solve kernels."""
+    import numpy as np
+    contact, _ = _batch(3, 2, n_mid=4)
+    bins = bench.bins_of(contact)
+    assert bins.tolist() == [1, 1, 1, 3, 3, 3, 3, 4, 4]
+    assert bench.kernel_of_bins(np.arange(5)).tolist() == [0, 0, 1, 1, 2]
 
 
 def test_roofline_dominant_and_critical_kernels():
-    """Two class kernels: the dominant one processes the most solves, the critical one has the
+    """Three kernels: the dominant one processes the most solves, the critical one has the
     longest live time (it sets the step); the HBM fraction is algorithmic bytes / live time."""
-    contact, iters = _batch(900, 100)
+    contact, iters = _batch(900, 100, n_mid=50)
     bins = bench.bins_of(contact)
-    plan = _StubPlan(["solve_group_kernel<128, 96, false>", "solve_group_kernel<192, 160, false>"])
-    roof, comp, crit = bench.kernel_roofline(plan, 1000, bins, contact, iters, [9.0, 12.0], [1, 1],
-                                             step_ms=12.5)
+    plan = _StubPlan(["solve_group_kernel<128, 96, false>", "solve_group_kernel<160, 144, false>",
+                      "solve_group_kernel<192, 0, false>"])
+    roof, comp, crit = bench.kernel_roofline(plan, 1050, bins, contact, iters, [9.0, 4.0, 12.0],
+                                             [1, 1, 1], step_ms=12.5)
     assert roof["kernel"].startswith("solve_group_kernel<128") and roof["solves_per_launch"] == 900
     assert crit["kernel"].startswith("solve_group_kernel<192") and crit["solves_per_launch"] == 100
+    assert roof["solves_per_kernel"]["solve_group_kernel<160, 144, false>"] == 50
     assert not crit["same_as_dominant"] and abs(crit["step_share"] - 12.0 / 12.5) < 1e-12
     assert abs(roof["achieved"] - bench.BYTES_PER_SOLVE * 900 / 9e-3 / 1e9) < 1e-9
     assert abs(crit["frac"] - bench.BYTES_PER_SOLVE * 100 / 12e-3 / 1e9 / bench.HBM_PEAK_GBS) < 1e-12
@@ -57,9 +69,9 @@ def test_roofline_dominant_and_critical_kernels():
 def test_roofline_single_kernel():
     """One solve kernel for every bin (pair kernel): dominant == critical, all solves counted."""
     contact, iters = _batch(900, 100)
-    plan = _StubPlan(["solve_pair_kernel<false>", None])
+    plan = _StubPlan(["solve_pair_kernel<false>", None, None])
     roof, comp, crit = bench.kernel_roofline(plan, 1000, bench.bins_of(contact), contact, iters,
-                                             [10.0, 0.0], [2, 0], step_ms=5.2)
+                                             [10.0, 0.0, 0.0], [2, 0, 0], step_ms=5.2)
     assert roof["kernel"] == crit["kernel"] == "solve_pair_kernel<false>"
     assert roof["solves_per_launch"] == 1000 and roof["kernel_avg_ms"] == 5.0
     assert crit["same_as_dominant"] and list(roof["kernel_avg_ms_all"]) == ["solve_pair_kernel<false>"]

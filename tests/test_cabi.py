@@ -62,6 +62,21 @@ def test_invalid_params_rejected_before_device(lib, field, value):
     assert "cmpc_plan_create" in lib.cmpc_last_error().decode()
 
 
+def test_default_build_has_no_interior_point_variants(lib):
+    """The product library carries only the kernels that run by default: asking for the
+    interior-point fallback (a -DCMPC_WITH_IPM variant build) is rejected before the device."""
+    import os
+    from cmpc import _lib
+    if os.environ.get("CMPC_LIB"):
+        pytest.skip("a variant library is loaded")
+    p = _lib.CParams()
+    lib.cmpc_params_default(ctypes.byref(p))
+    p.ipm_facts = 8
+    h = ctypes.c_void_p()
+    assert lib.cmpc_plan_create(ctypes.byref(p), ctypes.byref(h)) == -22
+    assert "CMPC_WITH_IPM" in lib.cmpc_last_error().decode()
+
+
 def test_null_arguments(lib):
     assert lib.cmpc_plan_create(None, None) == -22
     assert lib.cmpc_solve(None, 1, *([None] * 10)) == -22

@@ -61,7 +61,7 @@ def test_status_and_iters_sane(plan):
 
 def _bins(contact):
     nf = 3 * (contact != 0).reshape(contact.shape[0], -1).sum(1)
-    return np.searchsorted(np.array([96, 128, 160, 192]), nf)
+    return np.searchsorted(np.array([96, 128, 144, 160, 192]), nf)
 
 
 def test_heaviest_bin_parity(plan):
@@ -71,7 +71,7 @@ def test_heaviest_bin_parity(plan):
     from cmpc import solve_batch
     fx = load_fixture("qp_nc192.npz")
     batch = fixture_batch(fx)
-    assert np.all(_bins(batch["contact"]) == 3)
+    assert np.all(_bins(batch["contact"]) == 4)
     w, st, it = solve_batch(batch, plan=plan)
     assert np.all(st == 1), (st, it)
     err = rel_err_U(w, fx["w"])

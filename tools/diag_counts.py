@@ -57,7 +57,7 @@ def main():
                 print(f"  {R} ranks: shard max instance {max(x.max() for x in sh):.0f} cycles, "
                       f"mean per shard {np.mean([x.sum() for x in sh]):.3g}")
             nc = np.array([int(v) for v in d["contact"].reshape(65536, -1).ne(0).sum(1).cpu()]) * 3
-            for lo, hi in ((0, 96), (97, 128), (129, 160), (161, 192)):
+            for lo, hi in ((0, 96), (97, 128), (129, 144), (145, 160), (161, 192)):
                 m = (nc >= lo) & (nc <= hi)
                 if m.any():
                     print(f"  bin <= {hi}: {m.sum()} inst, mean cycles {cyc[m].mean():.0f}, "

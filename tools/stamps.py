@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--warm", action="store_true",
                     help="measure the bench's next-tick warm-start scenario (cold twin first)")
     ap.add_argument("--team", type=int, default=-1, help="cmpc_plan_set_team (-1 auto, 0 off)")
-    ap.add_argument("--only-bin", type=int, default=-1, help="keep only instances of this bin (0-3)")
+    ap.add_argument("--only-bin", type=int, default=-1, help="keep only instances of this bin (0-4)")
     a = ap.parse_args()
     import torch
     from cmpc import _lib, synth
@@ -32,7 +32,7 @@ def main():
     b = synth.make_batch(a.batch, seed=1, mixed=(a.config == 2))
     if a.only_bin >= 0:
         nf = 3 * (b["contact"] != 0).reshape(a.batch, -1).sum(1)
-        keep = np.searchsorted(np.array([96, 128, 160, 192]), nf) == a.only_bin
+        keep = np.searchsorted(np.array([96, 128, 144, 160, 192]), nf) == a.only_bin
         b = {k: (v[keep] if isinstance(v, np.ndarray) and v.shape[:1] == keep.shape else v) for k, v in b.items()}
         a.batch = int(keep.sum())
         print("instances kept:", a.batch)
@@ -75,6 +75,9 @@ def report(lib, plan, d, buf, kw, title):
             continue
         print(f"  {nm:28s} {v[i]/n:12.0f} cycles/instance  {100*v[i]/v[5]:5.1f}%")
     print(f"  per call: condense {v[0]/v[8]:.0f}  invert {v[1]/v[8]:.0f}  gradient {v[2]/max(v[12],1):.0f} (x{v[12]/n:.1f})  symv {v[3]/max(v[13],1):.0f} (x{v[13]/n:.1f}) cycles")
+    if v[29] > 0:
+        print(f"  face downdates: {v[29]/n:.3f} repairs/instance ({v[30]/v[29]:.2f} faces each), "
+              f"{v[28]/v[29]:.0f} cycles per repair, {100*v[28]/v[5]:.1f}% of the total")
     if v[16] + v[19] > 0:
         print(f"  team factor per call: backward {v[16]/v[8]:.0f}  forward {v[17]/v[8]:.0f}  "
               f"mirror+scale {v[18]/v[8]:.0f}  sweep {v[19]/v[8]:.0f} cycles")
