@@ -247,10 +247,20 @@ def kernel_roofline(plan, B_shard, bins, contact, iters, ms, calls, traffic=None
         achieved = BYTES_PER_SOLVE * n_k[k] / (avg[k] * 1e-3) / 1e9 if avg[k] > 0 else 0.0
         ck = None if team else _counters_of(counters, names[k])
         tr = ck.get("hbm_bytes_per_launch") if ck else (traffic if (k == q and not team) else None)
-        return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": tr, "kernel": names[k],
-                "kernel_avg_ms": avg[k], "solves_per_launch": n_k[k],
-                "bytes_per_solve": BYTES_PER_SOLVE}
+        tr_raw = ck.get("hbm_bytes_per_launch_raw") if ck else None
+        alg = BYTES_PER_SOLVE * n_k[k]
+        out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK_GBS, "traffic": tr, "kernel": names[k],
+               "kernel_avg_ms": avg[k], "solves_per_launch": n_k[k],
+               "bytes_per_solve": BYTES_PER_SOLVE}
+        if tr is not None or tr_raw is not None:
+            # PMC bytes per launch: `traffic` doubles FETCH_SIZE (the gfx950 correction, exact
+            # for 16-B/lane coalesced reads only), `traffic_raw` = FETCH_SIZE + WRITE_SIZE as
+            # counted; the kernel's narrow / scratch loads put the true HBM bytes between them
+            out.update(traffic_raw=tr_raw, algorithmic_bytes_per_launch=alg,
+                       traffic_over_algorithmic=(tr / alg if tr and alg else None),
+                       traffic_raw_over_algorithmic=(tr_raw / alg if tr_raw and alg else None))
+        return out
 
     def compute(k):
         fl = float(flops[kern == k].sum())

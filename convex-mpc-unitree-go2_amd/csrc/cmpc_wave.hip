@@ -713,13 +713,184 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
   WSYNC();
 }
 
-// Which condensation: the block-row form has ~25 % fewer MFMAs but longer dependency chains.
-// With one wave per SIMD (small batches, latency) the chains are what a wave waits on either way
-// and the fewer MFMAs win (B = 256: 0.61 -> 0.48 ms); with two busy waves per SIMD the
-// forward form keeps the matrix pipe ~80 % busy and is ~5 % faster (tools/phase_bench.hip).
+// Closed-form condensation for a nilpotent step matrix (round 4).  The reference discretises a
+// nilpotent Ac (Ac^2 = 0: its only blocks map velocity to position and omega to the Euler
+// rates), so its zero-order hold is exactly A = I + N with N = Ac dt and N^2 = 0
+// (com_trajectory.py:272-286; cmpc_build_dynamics).  Then A^j = I + j N and the
+// prediction column of param p (step k_p) at step t >= k_p is affine in t:
+//     A^{t - k_p} b_p = U_p + t V_p,   V_p = N b_p,   U_p = b_p - k_p V_p,
+// so  H[p][p'] = sum_{t >= m} (U_p + t V_p)' Q2 (U_p' + t V_p'),  m = max(k_p, k_p'),
+//              = X_p' U_p' + Y_p' V_p'   with   X_p = Q2 (S0 U_p + S1 V_p),
+//                                               Y_p = Q2 (S1 U_p + S2 V_p),
+// S_i = sum_{t=m}^{N-1} t^i, whenever m = k_p (the row param's step).  Params are ordered by
+// step, so that holds for every entry of an off-diagonal tile (rows later than columns) and for
+// the lower part of a diagonal tile; the rest of a diagonal tile is mirrored, as in the
+// block-row form.  Every tile is then SIX MFMAs (two K = 12 products, 3 each) instead of the
+// three per active step of the forward form: ~240 MFMAs for n = 120 instead of 1,248 (936 in
+// the block-row form), with V = N b three MFMAs per 16-param chunk, parked in the G slab.  fp32
+// error on the fixture matrices (unit-diagonal scaled, vs float64): 2.6e-7 against 4.1e-7 for
+// the step-by-step products.  The solve checks N^2 = 0 exactly per instance (nilpotent_step);
+// any other A takes the general forms above.
+template <int NC>
+__device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P,
+                                                   f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
+  using C = Cfg<NC>;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  const int N = P.N;
+  n = uniform(n);
+  const int TA = (n + 15) >> 4;
+#pragma unroll
+  for (int t = 0; t < C::NTL; ++t) M[t] = f4{0.f, 0.f, 0.f, 0.f};
+  float* Vs = s.G;  // V = N b, param-major [p][12] (the G slab is free while condensing)
+  {
+    // K = 12 state layout (as condense_tiles_fwd): accumulator position 4g + q holds state 3g + q
+    const int sc = ((c & 3) < 3) ? 3 * (c >> 2) + (c & 3) : -1;
+    float aN[3];  // A operand of N X: N[sc][3g + q]
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int r = 3 * g + q;
+      aN[q] = (sc >= 0) ? s.A[sc * 12 + r] - ((sc == r) ? 1.f : 0.f) : 0.f;
+    }
+    WSYNC();
+#pragma unroll
+    for (int J = 0; J < C::TT; ++J) {
+      if (J >= TA) continue;  // uniform
+      const int p = 16 * J + c;
+      float bt[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bt[q] = (p < n) ? s.Bt[p * kBS + 3 * g + q] : 0.f;
+      f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < 3; ++q) d = mfma4(aN[q], bt[q], d);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) Vs[p * 12 + 3 * g + q] = d[q];
+    }
+  }
+  WSYNC();
+  const float fN = (float)N;
+  const float s1N = 0.5f * fN * (fN - 1.f), s2N = (fN - 1.f) * fN * (2.f * fN - 1.f) / 6.f;
+  float q2[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) q2[q] = s.Q2[3 * g + q];
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    if (I >= TA) continue;  // uniform
+    float x[3], y[3];
+    {
+      const int p = 16 * I + c;
+      const bool ok = p < n;
+      const float kf = ok ? (float)s.par[p] : 0.f;
+      const float S0 = fN - kf;                                       // sum_{t=k}^{N-1} 1
+      const float S1 = s1N - 0.5f * kf * (kf - 1.f);                  // ... t
+      const float S2 = s2N - (kf - 1.f) * kf * (2.f * kf - 1.f) / 6.f;  // ... t^2
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const float v = ok ? Vs[p * 12 + 3 * g + q] : 0.f;
+        const float u = ok ? fmaf(-kf, v, s.Bt[p * kBS + 3 * g + q]) : 0.f;
+        x[q] = q2[q] * fmaf(S0, u, S1 * v);
+        y[q] = q2[q] * fmaf(S1, u, S2 * v);
+      }
+    }
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      const int p = 16 * J + c;
+      const bool ok = p < n;
+      const float kf = ok ? (float)s.par[p] : 0.f;
+      float u[3], v[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        v[q] = ok ? Vs[p * 12 + 3 * g + q] : 0.f;
+        u[q] = ok ? fmaf(-kf, v[q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
+      }
+      f4 acc = M[tile_index(I, J)];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) acc = mfma4(x[q], u[q], acc);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) acc = mfma4(y[q], v[q], acc);
+      M[tile_index(I, J)] = acc;
+    }
+  }
+  // diagonal tiles: entry (r, c) with step(c) > step(r) is the mirror of (c, r)
+  WSYNC();
+  float* T = s.G;  // 16 x 16 scratch per tile (V is dead)
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    if (I >= TA) continue;  // uniform
+    f4 v = M[tile_index(I, I)];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) T[(4 * g + q) * 16 + c] = v[q];
+    WSYNC();
+    const int pc = 16 * I + c;
+    const int kc = (pc < n) ? s.par[pc] : N;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int pr = 16 * I + 4 * g + q;
+      const int kr = (pr < n) ? s.par[pr] : N;
+      if (kc > kr) v[q] = T[c * 16 + 4 * g + q];
+    }
+    M[tile_index(I, I)] = v;
+    WSYNC();
+  }
+  // + diag(Rt) + shift, identity on padding
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      f4 v = M[tile_index(I, J)];
+      const int col = 16 * J + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
+        else if (row == col) v[q] += s.Rt[row] + shift;
+      }
+      M[tile_index(I, J)] = v;
+    }
+  }
+  WSYNC();
+}
+
+// Is the step matrix A = I + N with N^2 = 0 exactly (the reference's discretisation)?  Then
+// condense_tiles_nil applies.  Uniform.
+template <class SM>
+__device__ __forceinline__ bool nilpotent_step(SM& s) {
+  const int lane = opaque_lane();
+  WSYNC();
+  bool nz = false;
+#pragma unroll
+  for (int e0 = 0; e0 < 144; e0 += 64) {
+    const int e = e0 + lane;
+    if (e < 144) {
+      const int i = e / 12, j = e % 12;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        const float nik = s.A[i * 12 + k] - ((i == k) ? 1.f : 0.f);
+        const float nkj = s.A[k * 12 + j] - ((k == j) ? 1.f : 0.f);
+        acc = fmaf(nik, nkj, acc);
+      }
+      nz |= acc != 0.f;
+    }
+  }
+  return __any(nz) == 0;
+}
+
+// Which condensation: the closed form for a nilpotent step (nil); otherwise the block-row form
+// has ~25 % fewer MFMAs but longer dependency chains.  With one wave per SIMD (small batches,
+// latency) the chains are what a wave waits on either way and the fewer MFMAs win (B = 256:
+// 0.61 -> 0.48 ms); with two busy waves per SIMD the forward form keeps the matrix pipe ~80 %
+// busy and is ~5 % faster (tools/phase_bench.hip).
 template <int NC>
 __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
-                                               f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
+                                               f4 (&M)[Cfg<NC>::NTL], int n, float shift,
+                                               bool nil = false) {
+#ifndef CMPC_NO_NIL
+  if (nil) {  // uniform
+    condense_tiles_nil<NC>(s, P, M, n, shift);
+    return;
+  }
+#endif
   if constexpr (NC <= 128) {  // the 1-wave-per-SIMD bins would spill the second form
     if (P.latency_mode) {  // uniform
       condense_tiles_bc<NC>(s, P, M, n, shift);
@@ -1290,13 +1461,14 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   const int sy = (code & 8) ? 1 : ((code & 16) ? -1 : 0);
   const bool zl = (code & 1) != 0;
   if (owns) {
-    // the forces from the basis params (a face added by a downdate keeps its param, which the
-    // constraint holds on the face to rounding); the KKT conditions below use the current faces
+    // the forces on the current faces exactly (a face added by a downdate keeps its basis
+    // param, which the refinement holds on the face only to rounding -- up to 1e-2 N off in
+    // fp32 -- so the face's own value is taken, as for a face of the basis)
     const int pk = s.fpk[lane];
     const int px = pk & 255, py = (pk >> 8) & 255, pz = (pk >> 16) & 255;
-    fz = (pz == 255) ? fzmin : s.v[pz];
-    fx = (px == 255) ? sx * mu * fz : s.v[px];
-    fy = (py == 255) ? sy * mu * fz : s.v[py];
+    fz = zl ? fzmin : s.v[pz];
+    fx = (sx == 0) ? s.v[px] : sx * mu * fz;
+    fy = (sy == 0) ? s.v[py] : sy * mu * fz;
     const float* Bk = Bg + k * 144 + 3 * leg;
     float ax = 0.f, ay = 0.f, az = 0.f;
 #pragma unroll
@@ -1976,6 +2148,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     build_admm_basis<NC>(s, P, Bg, ntri);
   }
   const int n = 3 * ntri;
+  const bool nil = nilpotent_step(s);  // A = I + N, N^2 = 0: the closed-form condensation
   // team mode: the gradient's powers of A once per instance (registers to spare: the tiles are
   // split over the team)
   // (NC <= 128 only: the larger bins need those registers for their tiles)
@@ -2133,7 +2306,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #endif
       if constexpr (W == 1) {
         CMPC_T0(t_c);
-        condense_tiles<NC>(s, P, M, nact, uniformf(shift));
+        condense_tiles<NC>(s, P, M, nact, uniformf(shift), nil);
         CMPC_ACC(0, t_c);
         CMPC_T0(t_i);
         invert_tiles<NC>(s, M, nact);
