@@ -303,6 +303,7 @@ struct Smem {
   float R2[12];
   int par[NC];                     // param -> step k
   int off[kMaxN + 1];              // first param of step k
+  int nil;                         // A = I + N with N^2 = 0 (nilpotent_step): closed forms apply
   int tri[kMaxTri];                // stance triple t -> 4k + leg
   int tri_of[kMaxTri];             // 4k + leg -> triple index or -1
   int8_t tcnt[kMaxTri];            // polish: params of triple t / repaired face code
@@ -1118,6 +1119,7 @@ __device__ __forceinline__ void symv(SM& s, const f4 (&M)[Cfg<NC>::NTL], int n,
 // is the trajectory itself).  A^d and (A')^d come from repeated squaring in the same layout.
 // powers A^d and (A')^d, d = 1, 2, 4, 8, in accumulator layout over state positions
 // (pw[l][q] = A^(2^l)[state 3g+q][state of position c]); the gradient's scans use them
+// (nilpotent step, s.nil: A^d = I + d N exactly, no squaring)
 template <class SM>
 __device__ __forceinline__ void gradient_powers(SM& s, f4 (&pw)[4], f4 (&tw)[4]) {
   const int lane = opaque_lane();
@@ -1132,6 +1134,18 @@ __device__ __forceinline__ void gradient_powers(SM& s, f4 (&pw)[4], f4 (&tw)[4])
   }
   pw[0] = Pd;
   tw[0] = Td;
+  if (uniform(s.nil)) {
+#pragma unroll
+    for (int l = 1; l < 4; ++l) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float dl = (sc == 3 * g + q && q < 3) ? 1.f : 0.f;
+        pw[l][q] = fmaf((float)(1 << l), Pd[q] - dl, dl);
+        tw[l][q] = fmaf((float)(1 << l), Td[q] - dl, dl);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int l = 1; l < 4; ++l) {
     f4 pn = {0.f, 0.f, 0.f, 0.f}, tn = {0.f, 0.f, 0.f, 0.f};
@@ -1536,9 +1550,14 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   loose = (__all(lok) != 0) && step_ok;
   const bool all_ok = (__all(ok) != 0) && step_ok;
   if (all_ok && owns) {
-    s.x[3 * lane] = fx;
-    s.x[3 * lane + 1] = fy;
-    s.x[3 * lane + 2] = fz;
+    // onto the pyramid exactly: the check admits violations up to polish_tol x the force scale
+    // (~2e-3 N), the reference's bounds take none (a move of at most that, far inside the 1e-4
+    // parity bar)
+    float px, py, pz;
+    project(fx, fy, fz, mu, fzmin, px, py, pz);
+    s.x[3 * lane] = px;
+    s.x[3 * lane + 1] = py;
+    s.x[3 * lane + 2] = pz;
   }
   return all_ok;
 }
@@ -2149,6 +2168,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   }
   const int n = 3 * ntri;
   const bool nil = nilpotent_step(s);  // A = I + N, N^2 = 0: the closed-form condensation
+  if (lane == 0) s.nil = nil ? 1 : 0;   // (and the gradient's powers of A)
+  WSYNC();
   // team mode: the gradient's powers of A once per instance (registers to spare: the tiles are
   // split over the team)
   // (NC <= 128 only: the larger bins need those registers for their tiles)
@@ -2411,9 +2432,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       if (loose) {  // the session ends on a set within the loose tolerance: accept it
         const int l = opaque_lane();
         WSYNC();
-        if (l < ntri) {
-#pragma unroll
-          for (int a = 0; a < 3; ++a) s.x[3 * l + a] = s.dl[3 * l + a];
+        if (l < ntri) {  // (projected onto the pyramid: the loose check admits 5x polish_tol)
+          float px, py, pz;
+          project(s.dl[3 * l], s.dl[3 * l + 1], s.dl[3 * l + 2], P.mu, P.fz_min, px, py, pz);
+          s.x[3 * l] = px;
+          s.x[3 * l + 1] = py;
+          s.x[3 * l + 2] = pz;
         }
         polished = true;
         status = 1;

@@ -153,15 +153,16 @@ def test_class_order_independent():
 def test_full_size_certified_sample(plan):
     """The full config-3 batch (65,536 trot + mixed, the headline workload) in one solve: every
     instance status 1 and feasible, X the rollout of U, and 512 instances stratified over the
-    four bins (tests/golden/qp_cfg3.npz: 128 / 256 / 127 / 1 at NC 96 / 128 / 160 / 192) within
-    1e-4 of their KKT-certified optimum."""
+    bins (tests/golden/qp_cfg3.npz: 128 / 256 / 87 / 40 / 1 at NC 96 / 128 / 144 / 160 / 192 --
+    drawn as 128 / 256 / 127 / 1 over round 1's four bins, whose NC 160 bin now splits into two)
+    within 1e-4 of their KKT-certified optimum."""
     from cmpc import solve_batch, synth
     from parity_util import input_digest
     fx = load_fixture("qp_cfg3.npz")
     b = synth.make_config(3, B=65536)
     idx = fx["idx"]
     assert input_digest(b, idx) == str(fx["digest"]), "config-3 generator drifted"
-    assert np.array_equal(np.bincount(_bins(b["contact"][idx]), minlength=4), [128, 256, 127, 1])
+    assert np.array_equal(np.bincount(_bins(b["contact"][idx]), minlength=5), [128, 256, 87, 40, 1])
     w, st, it = solve_batch(b, plan=plan)
     assert np.all(np.isfinite(w))
     assert np.all(st == 1), np.unique(st, return_counts=True)
