@@ -272,8 +272,85 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
     aT[q] = (sc >= 0) ? s.A[r * 12 + sc] : 0.f;
     q2[q] = (r == sc) ? s.Q2[r] : 0.f;
   }
-  float* Cs = s.G;  // C_i columns, param-major [p][12]
+  float* Cs = s.G;  // C_i columns (or V = N b: the closed form), param-major [p][12]
   CMPC_T0(t_f0);
+  if (uniform(s.nil)) {
+    // ---- closed form for a nilpotent step (cmpc_wave.hip condense_tiles_nil): V = N b by the
+    // chunk's wave (J % W), one barrier, then every owned tile is six MFMAs
+    {
+      float aN[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const int r = 3 * g + q;
+        aN[q] = (sc >= 0) ? s.A[sc * 12 + r] - ((sc == r) ? 1.f : 0.f) : 0.f;
+      }
+#pragma unroll
+      for (int J = 0; J < TT; ++J) {
+        if (J % W != w) continue;  // uniform
+        if (16 * J >= n) continue;  // uniform
+        const int p = 16 * J + c;
+        float bt[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bt[q] = (p < n) ? s.Bt[p * kBS + 3 * g + q] : 0.f;
+        f4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 3; ++q) d = mfma4(aN[q], bt[q], d);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) Cs[p * 12 + 3 * g + q] = d[q];
+      }
+    }
+    team_barrier();  // every V chunk in LDS
+    CMPC_ACC(16, t_f0);
+    CMPC_T0(t_f1);
+    const float fN = (float)N;
+    const float s1N = 0.5f * fN * (fN - 1.f), s2N = (fN - 1.f) * fN * (2.f * fN - 1.f) / 6.f;
+    float qd[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) qd[q] = s.Q2[3 * g + q];
+#pragma unroll
+    for (int j = 0; j < T::PPW; ++j) {
+      const int pr = w + j * W;
+      if (pr >= T::NPAIR) continue;  // uniform
+#pragma unroll
+      for (int l = 0; l <= TT; ++l) {
+        int I, J;
+        team_slot<NC, W>(w, j, l, I, J);
+        if (16 * I >= n) continue;  // uniform: padding rows stay zero
+        float x[3], y[3], u[3], v[3];
+        {
+          const int p = 16 * I + c;
+          const bool ok = p < n;
+          const float kf = ok ? (float)s.par[p] : 0.f;
+          const float S0 = fN - kf, S1 = s1N - 0.5f * kf * (kf - 1.f);
+          const float S2 = s2N - (kf - 1.f) * kf * (2.f * kf - 1.f) / 6.f;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            const float vv = ok ? Cs[p * 12 + 3 * g + q] : 0.f;
+            const float uu = ok ? fmaf(-kf, vv, s.Bt[p * kBS + 3 * g + q]) : 0.f;
+            x[q] = qd[q] * fmaf(S0, uu, S1 * vv);
+            y[q] = qd[q] * fmaf(S1, uu, S2 * vv);
+          }
+        }
+        {
+          const int p = 16 * J + c;
+          const bool ok = p < n;
+          const float kf = ok ? (float)s.par[p] : 0.f;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            v[q] = ok ? Cs[p * 12 + 3 * g + q] : 0.f;
+            u[q] = ok ? fmaf(-kf, v[q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
+          }
+        }
+        f4 acc = M[j * (TT + 1) + l];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc = mfma4(x[q], u[q], acc);
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc = mfma4(y[q], v[q], acc);
+        M[j * (TT + 1) + l] = acc;
+      }
+    }
+    CMPC_ACC(17, t_f1);
+  } else {
   // ---- backward: P_i (every wave, registers) and C_i = P_i B_i (chunk J written by wave J % W)
   {
     f4 Pt = q2;
@@ -395,6 +472,7 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
     }
   }
   CMPC_ACC(17, t_f1);
+  }  // (general A)
   CMPC_T0(t_f2);
   // ---- diagonal tiles: entry (r, c) with step(c) > step(r) is the mirror of (c, r); then
   // + diag(Rt) + shift, identity on padding; the sweep's scaling from the diagonals.  A pair's

@@ -190,3 +190,26 @@ def test_check_termination_reference_interval():
         assert np.all(it % 10 == 0) and it.min() >= 10, np.unique(it)
         err = rel_err_U(w, np.repeat(fx["w"], reps, axis=0))
         assert err.max() <= TOL_U, err.max()
+
+
+@pytest.mark.parametrize("reps", [1, 1100])
+def test_general_step_matrix(plan, reps):
+    """A step matrix that is NOT I + N with N^2 = 0 takes the general condensation and the
+    gradient's squared powers of A (the reference's nilpotent ZOH takes the closed forms,
+    cmpc_wave.hip condense_tiles_nil): a perturbed Ad (an attitude-damping term on the Euler
+    rates, A[3:6, 3:6] = 0.999 I) is solved to 1e-4 of ITS certified optimum, in latency mode and
+    replicated past the latency threshold (throughput mode)."""
+    from cmpc import solve_batch, synth
+    b = synth.make_config(2, B=8)
+    for i in range(8):
+        for r in range(3, 6):
+            b["Ad"][i, r, r] = 0.999
+    Nm = b["Ad"][0].astype(np.float32) - np.eye(12, dtype=np.float32)
+    assert np.any(Nm @ Nm != 0)  # not nilpotent: the general path
+    big = {k: np.repeat(v, reps, axis=0) for k, v in b.items() if isinstance(v, np.ndarray)
+           and v.shape[:1] == (8,)}
+    w, st, it = solve_batch(big, plan=plan)
+    assert np.all(st == 1), np.unique(st, return_counts=True)
+    for i in range(8):
+        wr = _tight(b, i)
+        assert rel_err_U(w[i * reps:i * reps + 1], wr[None])[0] <= TOL_U, i

@@ -40,3 +40,26 @@ def test_algorithm_model_reaches_parity():
         assert out["status"] == 1
         w = np.concatenate([np.zeros(192), out["U"].reshape(-1)])
         assert rel_err_U(w[None], fx["w"][i:i + 1])[0] < 1e-4
+
+
+def test_algorithm_model_face_downdates():
+    """tests/algo_spec.py with the kernel's face downdates (cmpc_wave.hip face_downdate) and its
+    fp32 sweep inverse: the same certified optima, and the pure face-adding repairs skip their
+    factorization (hard fixture instances, which repair)."""
+    import algo_spec
+    from parity_util import load_fixture, fixture_batch, rel_err_U
+    fx = load_fixture("qp_hard.npz")
+    fb = fixture_batch(fx)
+    dd_reps = 0
+    facts = [0, 0]
+    for i in range(len(fx["w"])):
+        inst = {k: v[i] for k, v in fb.items()}
+        base = algo_spec.solve(inst, algo_spec.Params(fp32_polish=True))
+        out = algo_spec.solve(inst, algo_spec.Params(fp32_polish=True, downdate=True, dd_max=6))
+        assert out["status"] == 1
+        w = np.concatenate([np.zeros(192), out["U"].reshape(-1)])
+        assert rel_err_U(w[None], fx["w"][i:i + 1])[0] < 1e-4
+        dd_reps += out["dd_repairs"]
+        facts[0] += base["fact"]
+        facts[1] += out["fact"]
+    assert dd_reps > 0 and facts[1] < facts[0], (dd_reps, facts)
