@@ -446,50 +446,6 @@ __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL]
   WSYNC();
 }
 
-// D = L diag(1 / i) L' of a symmetric 4x4 block (row-major Dm, lower part read), unit lower L
-struct Ldl4 {
-  float i0, i1, i2, i3;            // reciprocal pivots
-  float l10, l20, l30, l21, l31, l32;
-};
-__device__ __forceinline__ Ldl4 ldl4(const float (&Dm)[16]) {
-  Ldl4 f;
-  f.i0 = __builtin_amdgcn_rcpf(Dm[0]);
-  f.l10 = Dm[4] * f.i0; f.l20 = Dm[8] * f.i0; f.l30 = Dm[12] * f.i0;
-  f.i1 = __builtin_amdgcn_rcpf(Dm[5] - f.l10 * Dm[4]);
-  const float u21 = Dm[9] - f.l20 * Dm[4], u31 = Dm[13] - f.l30 * Dm[4];
-  f.l21 = u21 * f.i1; f.l31 = u31 * f.i1;
-  f.i2 = __builtin_amdgcn_rcpf(Dm[10] - f.l20 * Dm[8] - f.l21 * u21);
-  const float u32 = Dm[14] - f.l30 * Dm[8] - f.l31 * u21;
-  f.l32 = u32 * f.i2;
-  f.i3 = __builtin_amdgcn_rcpf(Dm[15] - f.l30 * Dm[12] - f.l31 * u31 - f.l32 * u32);
-  return f;
-}
-
-// The rank-4 MFMA operands of Y diag(1 / dl) Y' with Y = P^ L^-T for panel rows ph[I] (row
-// 16 I + c of the 4-column panel): a[I] = -Y[16 I + c][g], b[I] = Y[16 I + c][g] / dl_g
-template <int NC>
-__device__ __forceinline__ void ldl4_operands(const Ldl4& f, const f4 (&ph)[Cfg<NC>::TT], int g,
-                                              float (&a)[Cfg<NC>::TT], float (&b)[Cfg<NC>::TT]) {
-  using C = Cfg<NC>;
-  const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
-  // y_g = (P^ L^-T)_g = sum_m L^-1[g][m] P^_m: this lane's row of L^-1 (unit lower) and
-  // 1/dl_g, selected once per step, so each panel row costs four FMAs and no branches
-  const float n10 = -f.l10, n21 = -f.l21, n32 = -f.l32;
-  const float n20 = f.l21 * f.l10 - f.l20, n31 = f.l32 * f.l21 - f.l31;
-  const float n30 = -f.l30 - f.l31 * n10 - f.l32 * n20;
-  const float w0 = g3 ? n30 : g2 ? n20 : g1 ? n10 : 1.f;
-  const float w1 = g3 ? n31 : g2 ? n21 : g1 ? 1.f : 0.f;
-  const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
-  const float w3 = g3 ? 1.f : 0.f;
-  const float ig = g3 ? f.i3 : g2 ? f.i2 : g1 ? f.i1 : f.i0;
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
-    const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
-    a[I] = -yg;
-    b[I] = yg * ig;
-  }
-}
-
 // LDL of the 4x4 pivot block (rows k0..k0+3 of the panel) and the step's MFMA operands
 template <int NC, class SM>
 __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
@@ -505,7 +461,32 @@ __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
   f4 ph[C::TT];
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
-  ldl4_operands<NC>(ldl4(Dm), ph, g, a, b);
+  // (inline: factored into a helper returning a struct, the compiler spilled an operand in
+  // every sweep step, 28 scratch stores and loads in the NC <= 128 kernel)
+  const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
+  const float i0 = __builtin_amdgcn_rcpf(Dm[0]);
+  const float l10 = Dm[4] * i0, l20 = Dm[8] * i0, l30 = Dm[12] * i0;
+  const float i1 = __builtin_amdgcn_rcpf(Dm[5] - l10 * Dm[4]);
+  const float u21 = Dm[9] - l20 * Dm[4], u31 = Dm[13] - l30 * Dm[4];
+  const float l21 = u21 * i1, l31 = u31 * i1;
+  const float i2 = __builtin_amdgcn_rcpf(Dm[10] - l20 * Dm[8] - l21 * u21);
+  const float u32 = Dm[14] - l30 * Dm[8] - l31 * u21;
+  const float l32 = u32 * i2;
+  const float i3 = __builtin_amdgcn_rcpf(Dm[15] - l30 * Dm[12] - l31 * u31 - l32 * u32);
+  const float n10 = -l10, n21 = -l21, n32 = -l32;
+  const float n20 = l21 * l10 - l20, n31 = l32 * l21 - l31;
+  const float n30 = -l30 - l31 * n10 - l32 * n20;
+  const float w0 = g3 ? n30 : g2 ? n20 : g1 ? n10 : 1.f;
+  const float w1 = g3 ? n31 : g2 ? n21 : g1 ? 1.f : 0.f;
+  const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
+  const float w3 = g3 ? 1.f : 0.f;
+  const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
+    a[I] = -yg;
+    b[I] = yg * ig;
+  }
 }
 
 // rank-4 update of the tiles whose criticality for pivot block Kc is CRIT
