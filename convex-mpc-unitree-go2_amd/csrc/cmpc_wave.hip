@@ -327,6 +327,34 @@ __device__ __forceinline__ constexpr int tile_index(int I, int J) { return (I * 
 // MFMAs per chunk, and every lower tile (I, J) accumulates (Q2 G_t)_I' (G_t)_J with four MFMAs
 // whose accumulator IS the matrix tile.  Tile row I starts to receive terms at the step of its
 // first parameter; nothing of G ever goes through memory.
+// + diag(Rt) + shift, identity on padding.  Only the diagonal tiles and the tile rows that reach
+// the padding (a lower tile's padded columns imply padded rows) have anything to change: the
+// interior off-diagonal tiles are skipped by a uniform test instead of testing every element.
+template <int NC>
+__device__ __forceinline__ void condense_finish(Smem<NC>& s, f4 (&M)[Cfg<NC>::NTL], int n,
+                                                float shift) {
+  using C = Cfg<NC>;
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+#pragma unroll
+    for (int J = 0; J <= I; ++J) {
+      if (J != I && 16 * I + 16 <= n) continue;  // uniform: interior off-diagonal tile
+      f4 v = M[tile_index(I, J)];
+      const int col = 16 * J + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = 16 * I + 4 * g + q;
+        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
+        else if (row == col) v[q] += s.Rt[row] + shift;
+      }
+      M[tile_index(I, J)] = v;
+    }
+  }
+  WSYNC();
+}
+
 template <int NC>
 __device__ __forceinline__ void condense_tiles_fwd(Smem<NC>& s, const KParams& P,
                                                    f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
@@ -391,23 +419,7 @@ __device__ __forceinline__ void condense_tiles_fwd(Smem<NC>& s, const KParams& P
       }
     }
   }
-  // + diag(Rt) + shift, identity on padding
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
-#pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      f4 v = M[tile_index(I, J)];
-      const int col = 16 * J + c;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = 16 * I + 4 * g + q;
-        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
-        else if (row == col) v[q] += s.Rt[row] + shift;
-      }
-      M[tile_index(I, J)] = v;
-    }
-  }
-  WSYNC();
+  condense_finish<NC>(s, M, n, shift);
 }
 
 // ---- software-pipelined sweep (bins up to kSweepPipeMaxNC; measured +3-5 % on NC = 128, and
@@ -676,23 +688,7 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
     M[tile_index(I, I)] = v;
     WSYNC();
   }
-  // + diag(Rt) + shift, identity on padding
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
-#pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      f4 v = M[tile_index(I, J)];
-      const int col = 16 * J + c;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = 16 * I + 4 * g + q;
-        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
-        else if (row == col) v[q] += s.Rt[row] + shift;
-      }
-      M[tile_index(I, J)] = v;
-    }
-  }
-  WSYNC();
+  condense_finish<NC>(s, M, n, shift);
 }
 
 // Closed-form condensation for a nilpotent step matrix (round 4).  The reference discretises a
@@ -755,6 +751,21 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
   float q2[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) q2[q] = s.Q2[3 * g + q];
+#ifdef CMPC_NIL_CACHE
+  // the column operands (u, v) of every chunk, once: each is reused by every tile row below it
+  float uc[C::TT][3], vc[C::TT][3];
+#pragma unroll
+  for (int J = 0; J < C::TT; ++J) {
+    const int p = 16 * J + c;
+    const bool ok = J < TA && p < n;
+    const float kf = ok ? (float)s.par[p] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      vc[J][q] = ok ? Vs[p * 12 + 3 * g + q] : 0.f;
+      uc[J][q] = ok ? fmaf(-kf, vc[J][q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
+    }
+  }
+#endif
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) {
     if (I >= TA) continue;  // uniform
@@ -776,15 +787,23 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
     }
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
+      float u[3], v[3];
+#ifdef CMPC_NIL_CACHE
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        u[q] = uc[J][q];
+        v[q] = vc[J][q];
+      }
+#else
       const int p = 16 * J + c;
       const bool ok = p < n;
       const float kf = ok ? (float)s.par[p] : 0.f;
-      float u[3], v[3];
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         v[q] = ok ? Vs[p * 12 + 3 * g + q] : 0.f;
         u[q] = ok ? fmaf(-kf, v[q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
       }
+#endif
       f4 acc = M[tile_index(I, J)];
 #pragma unroll
       for (int q = 0; q < 3; ++q) acc = mfma4(x[q], u[q], acc);
@@ -814,23 +833,7 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
     M[tile_index(I, I)] = v;
     WSYNC();
   }
-  // + diag(Rt) + shift, identity on padding
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
-#pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      f4 v = M[tile_index(I, J)];
-      const int col = 16 * J + c;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int row = 16 * I + 4 * g + q;
-        if (row >= n || col >= n) v[q] = (row == col) ? 1.f : 0.f;
-        else if (row == col) v[q] += s.Rt[row] + shift;
-      }
-      M[tile_index(I, J)] = v;
-    }
-  }
-  WSYNC();
+  condense_finish<NC>(s, M, n, shift);
 }
 
 // Is the step matrix A = I + N with N^2 = 0 exactly (the reference's discretisation)?  Then
