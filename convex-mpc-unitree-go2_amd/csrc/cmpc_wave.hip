@@ -751,8 +751,9 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
   float q2[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) q2[q] = s.Q2[3 * g + q];
-#ifdef CMPC_NIL_CACHE
   // the column operands (u, v) of every chunk, once: each is reused by every tile row below it
+  // (loaded per tile instead: 7 LDS reads between every tile's MFMAs; caching them took config 3
+  // 9.09 -> 8.60 ms, config 2 at 65,536 10.55 -> 9.99 ms, A/B in one gpurun call)
   float uc[C::TT][3], vc[C::TT][3];
 #pragma unroll
   for (int J = 0; J < C::TT; ++J) {
@@ -765,7 +766,6 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
       uc[J][q] = ok ? fmaf(-kf, vc[J][q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
     }
   }
-#endif
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) {
     if (I >= TA) continue;  // uniform
@@ -788,22 +788,11 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
       float u[3], v[3];
-#ifdef CMPC_NIL_CACHE
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         u[q] = uc[J][q];
         v[q] = vc[J][q];
       }
-#else
-      const int p = 16 * J + c;
-      const bool ok = p < n;
-      const float kf = ok ? (float)s.par[p] : 0.f;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        v[q] = ok ? Vs[p * 12 + 3 * g + q] : 0.f;
-        u[q] = ok ? fmaf(-kf, v[q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
-      }
-#endif
       f4 acc = M[tile_index(I, J)];
 #pragma unroll
       for (int q = 0; q < 3; ++q) acc = mfma4(x[q], u[q], acc);
