@@ -1,9 +1,12 @@
 #!/bin/bash
 # Build a variant of libcmpc.so with extra compile flags (A/B experiments).
 #   usage: bash scripts/build_variant.sh <name> [-DFLAG ...]  -> cmpc/lib/libcmpc_<name>.so
+#   (NO_VFORM=1: without -amdgpu-mfma-vgpr-form, which crashes the compiler on the interior-point
+#    kernel variants: bash scripts/build_variant.sh ipm -DCMPC_WITH_IPM with NO_VFORM=1)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form "$@" \
+VFORM="-mllvm -amdgpu-mfma-vgpr-form"; [ "${NO_VFORM:-0}" = "1" ] && VFORM=""
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -fno-slp-vectorize ${VFORM} "$@" \
   -Iinclude -Iconvex-mpc-unitree-go2_amd/csrc convex-mpc-unitree-go2_amd/csrc/cmpc_host.hip \
   -o convex-mpc-unitree-go2_amd/cmpc/lib/libcmpc_$name.so
