@@ -302,8 +302,6 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
     team_barrier();  // every V chunk in LDS
     CMPC_ACC(16, t_f0);
     CMPC_T0(t_f1);
-    const float fN = (float)N;
-    const float s1N = 0.5f * fN * (fN - 1.f), s2N = (fN - 1.f) * fN * (2.f * fN - 1.f) / 6.f;
     float qd[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q) qd[q] = s.Q2[3 * g + q];
@@ -311,6 +309,19 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
     for (int j = 0; j < T::PPW; ++j) {
       const int pr = w + j * W;
       if (pr >= T::NPAIR) continue;  // uniform
+      // the pair's two columns' operands, once (every slot of the pair reuses one of them)
+      float uc[2][3], vc[2][3];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = 16 * (h ? TT - 1 - pr : pr) + c;
+        const bool ok = p < n;
+        const float kf = ok ? (float)s.par[p] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          vc[h][q] = ok ? Cs[p * 12 + 3 * g + q] : 0.f;
+          uc[h][q] = ok ? fmaf(-kf, vc[h][q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
+        }
+      }
 #pragma unroll
       for (int l = 0; l <= TT; ++l) {
         int I, J;
@@ -320,9 +331,10 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
         {
           const int p = 16 * I + c;
           const bool ok = p < n;
-          const float kf = ok ? (float)s.par[p] : 0.f;
-          const float S0 = fN - kf, S1 = s1N - 0.5f * kf * (kf - 1.f);
-          const float S2 = s2N - (kf - 1.f) * kf * (2.f * kf - 1.f) / 6.f;
+          const int k = ok ? s.par[p] : 0;
+          const float kf = (float)k;
+          float S0, S1, S2;
+          step_sums(k, N, S0, S1, S2);
 #pragma unroll
           for (int q = 0; q < 3; ++q) {
             const float vv = ok ? Cs[p * 12 + 3 * g + q] : 0.f;
@@ -332,13 +344,11 @@ __device__ __forceinline__ void team_factor(Smem<NC>& s, TeamSmem<NC, W>& ts, co
           }
         }
         {
-          const int p = 16 * J + c;
-          const bool ok = p < n;
-          const float kf = ok ? (float)s.par[p] : 0.f;
+          const int h = (l < TT - pr) ? 0 : 1;  // (compile-time after unrolling)
 #pragma unroll
           for (int q = 0; q < 3; ++q) {
-            v[q] = ok ? Cs[p * 12 + 3 * g + q] : 0.f;
-            u[q] = ok ? fmaf(-kf, v[q], s.Bt[p * kBS + 3 * g + q]) : 0.f;
+            v[q] = vc[h][q];
+            u[q] = uc[h][q];
           }
         }
         f4 acc = M[j * (TT + 1) + l];

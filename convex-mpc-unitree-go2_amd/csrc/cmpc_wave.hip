@@ -709,6 +709,14 @@ __device__ __forceinline__ void condense_tiles_bc(Smem<NC>& s, const KParams& P,
 // error on the fixture matrices (unit-diagonal scaled, vs float64): 2.6e-7 against 4.1e-7 for
 // the step-by-step products.  The solve checks N^2 = 0 exactly per instance (nilpotent_step);
 // any other A takes the general forms above.
+// Sums over the horizon's remaining steps t = k .. N-1 of 1, t and t^2 (condense_tiles_nil), as
+// exact integers
+__device__ __forceinline__ void step_sums(int k, int N, float& S0, float& S1, float& S2) {
+  S0 = (float)(N - k);
+  S1 = (float)((N * (N - 1) - k * (k - 1)) >> 1);
+  S2 = (float)(((N - 1) * N * (2 * N - 1) - (k - 1) * k * (2 * k - 1)) / 6);
+}
+
 template <int NC>
 __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P,
                                                    f4 (&M)[Cfg<NC>::NTL], int n, float shift) {
@@ -746,8 +754,6 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
     }
   }
   WSYNC();
-  const float fN = (float)N;
-  const float s1N = 0.5f * fN * (fN - 1.f), s2N = (fN - 1.f) * fN * (2.f * fN - 1.f) / 6.f;
   float q2[3];
 #pragma unroll
   for (int q = 0; q < 3; ++q) q2[q] = s.Q2[3 * g + q];
@@ -773,10 +779,10 @@ __device__ __forceinline__ void condense_tiles_nil(Smem<NC>& s, const KParams& P
     {
       const int p = 16 * I + c;
       const bool ok = p < n;
-      const float kf = ok ? (float)s.par[p] : 0.f;
-      const float S0 = fN - kf;                                       // sum_{t=k}^{N-1} 1
-      const float S1 = s1N - 0.5f * kf * (kf - 1.f);                  // ... t
-      const float S2 = s2N - (kf - 1.f) * kf * (2.f * kf - 1.f) / 6.f;  // ... t^2
+      const int k = ok ? s.par[p] : 0;
+      const float kf = (float)k;
+      float S0, S1, S2;  // sum_{t=k}^{N-1} 1, t, t^2
+      step_sums(k, N, S0, S1, S2);
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
         const float v = ok ? Vs[p * 12 + 3 * g + q] : 0.f;
