@@ -35,7 +35,8 @@ struct cmpc_plan {
   size_t slab[kNumGroups];   // park slab per wave (floats)
   // small batches (B <= team_max_batch): one kernel for all bins, kTeamWaves waves per QP
   // (cmpc_team.hip), on the caller's stream
-  int team_grid = 0;
+  int team_grid = 0;    // workgroups resident at two per CU (solve_team_kernel<W, 2>)
+  int team_grid1 = 0;   // at one per CU (<W, 1>: B <= CUs)
   size_t team_slab = 0;
   int64_t team_max_batch = -1;  // -1: automatic (B <= 4 x CUs: at most one wave per SIMD)
   // tail-bound batches (B <= ipm_max_batch): the one-wave kernel variants with the
@@ -248,11 +249,15 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   }
   {
     int nb = 0;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc::solve_team_kernel<kTeamWaves>,
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc::solve_team_kernel<kTeamWaves, 2>,
                                                      64 * kTeamWaves, 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) nb = 1;
     pl->team_grid = nb * cus;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc::solve_team_kernel<kTeamWaves, 1>,
+                                                     64 * kTeamWaves, 0);
+    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
+    pl->team_grid1 = nb < 1 ? 1 : nb > 1 ? cus : nb * cus;
     pl->team_slab = std::max({cmpc::TeamCfg<192, kTeamWaves>::SLAB, cmpc::TeamCfg<160, kTeamWaves>::SLAB,
                               cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB});
     work_floats = std::max(work_floats, (size_t)pl->team_grid * pl->team_slab);
@@ -375,6 +380,16 @@ static int64_t team_batch(const cmpc_plan* pl) {
   return pl->team_max_batch >= 0 ? pl->team_max_batch : 4LL * pl->cus;
 }
 
+// B <= CUs: every QP has a CU of its own, so the team kernel built for one workgroup per CU
+// runs (CMPC_TEAM_OCC=2 forces the two-per-CU image, for A/B)
+static bool team_one_per_cu(const cmpc_plan* pl, int64_t B) {
+  static const int occ = [] {
+    const char* v = getenv("CMPC_TEAM_OCC");
+    return v ? atoi(v) : 0;
+  }();
+  return occ != 2 && B <= pl->team_grid1;
+}
+
 // team mode: one launch for every bin; timed as solve kernel 0 (kernel 1 records no call)
 static int record_team_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams& kp,
                               const cmpc::Inputs& in, const cmpc::Outputs& out, int64_t B) {
@@ -392,10 +407,18 @@ static int record_team_launch(cmpc_plan* pl, hipStream_t s, const cmpc::KParams&
     }
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
-  const unsigned g = (unsigned)(pl->team_grid < B ? pl->team_grid : B);
-  hipLaunchKernelGGL(cmpc::solve_team_kernel<kTeamWaves>, dim3(g), dim3(64 * kTeamWaves), 0, s,
-                     kp, in, out, pl->d_lists, (int64_t)pl->p.max_batch, pl->d_counters,
-                     pl->d_counters + cmpc::kNumBins, pl->d_work, pl->team_slab);
+  // one QP per CU: the one-workgroup-per-CU image (512 registers per lane, no spills)
+  if (team_one_per_cu(pl, B)) {
+    const unsigned g = (unsigned)(pl->team_grid1 < B ? pl->team_grid1 : B);
+    hipLaunchKernelGGL((cmpc::solve_team_kernel<kTeamWaves, 1>), dim3(g), dim3(64 * kTeamWaves), 0,
+                       s, kp, in, out, pl->d_lists, (int64_t)pl->p.max_batch, pl->d_counters,
+                       pl->d_counters + cmpc::kNumBins, pl->d_work, pl->team_slab);
+  } else {
+    const unsigned g = (unsigned)(pl->team_grid < B ? pl->team_grid : B);
+    hipLaunchKernelGGL((cmpc::solve_team_kernel<kTeamWaves, 2>), dim3(g), dim3(64 * kTeamWaves), 0,
+                       s, kp, in, out, pl->d_lists, (int64_t)pl->p.max_batch, pl->d_counters,
+                       pl->d_counters + cmpc::kNumBins, pl->d_work, pl->team_slab);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "solve_team_kernel launch");
   if (rec_this) {
@@ -629,7 +652,8 @@ int cmpc_plan_heavy_first_batch(const cmpc_plan* pl, int64_t* min_batch) {
 
 const char* cmpc_plan_solve_kernel(const cmpc_plan* pl, int64_t B, int k) {
   if (!pl || B < 1 || k < 0 || k >= kNumGroups) return nullptr;
-  if (B <= team_batch(pl)) return k == 0 ? "solve_team_kernel<4>" : nullptr;
+  if (B <= team_batch(pl))
+    return k != 0 ? nullptr : team_one_per_cu(pl, B) ? "solve_team_kernel<4, 1>" : "solve_team_kernel<4, 2>";
   const bool ipm = kHasIpm && pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
   if (!has_group(pl, k)) return nullptr;
   return group_name(k, ipm);

@@ -2895,11 +2895,12 @@ __global__ void __launch_bounds__(64, Cfg<NCA>::WPE)
 
 // Team mode (cmpc_team.hip): one workgroup of W waves per QP, one kernel for all five bins
 // (heaviest first: the slow instances start first).  Wave 0 leads (drain loop +
-// solve_instance), waves 1..W-1 serve its matrix commands; at most two workgroups per CU
-// (<= 256 VGPRs per wave: the tiles are split W ways, so every bin fits the same class and a
-// small batch needs one launch on the caller's stream, no fork/join).
-template <int W>
-__global__ void __launch_bounds__(64 * W, 2)
+// solve_instance), waves 1..W-1 serve its matrix commands; the tiles are split W ways, so
+// every bin fits the same register class and a small batch needs one launch on the caller's
+// stream, no fork/join.  OCC = workgroups per CU: 2 (<= 256 registers per lane) for B > CUs,
+// 1 (<= 512: no spills) when every QP has a CU of its own.
+template <int W, int OCC>
+__global__ void __launch_bounds__(64 * W, OCC)
     solve_team_kernel(KParams P, Inputs in, Outputs out, const int* __restrict__ lists,
                       int64_t stride, const int* __restrict__ counts, int* __restrict__ heads,
                       float* __restrict__ work, size_t slab) {

@@ -247,7 +247,8 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
 /* Measurement hooks (not on the reference's interface; used by bench.py).  A solve launches at
  * most CMPC_NUM_SOLVE_KERNELS persistent solve kernels; cmpc_plan_solve_kernel names solve
  * kernel k (0, 1 or 2) of a batch of B instances, or returns NULL if that slot is not launched:
- *   B <= cmpc_plan_team_batch:  "solve_team_kernel<4>" (k = 0 only);
+ *   B <= cmpc_plan_team_batch:  "solve_team_kernel<4, 1>" (B <= CUs: one workgroup per CU)
+ *                               or "solve_team_kernel<4, 2>" (k = 0 only);
  *   larger batches:             "solve_group_kernel<128, 96, IPM>" (k = 0, the NC <= 128
  *                               class), "solve_group_kernel<160, 144, IPM>" (k = 1, the
  *                               NC 144 / 160 class; NULL if N is too short to need it) and

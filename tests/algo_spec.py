@@ -17,7 +17,9 @@ class Params:
                  eps_abs=1e-4, eps_rel=1e-4, polish_refine=4, tol_polish=1e-5, repairs=6,
                  fail_rho=4.0, late_repairs=3, backoff_cap=3, repair_top=2,
                  repair_top_from=1, repair_top_rep=2, repair_frac=0.5, stable_grow=3,
-                 fp32_polish=False, downdate=False, dd_max=24, hook=None):
+                 fp32_polish=False, downdate=False, dd_max=24, dd_rebase=False, hook=None,
+                 trace=None, fp32_admm=False, border_max=0, weak_base=0.0, border=0,
+                 border_extra=4, border_refine=0):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -37,7 +39,19 @@ class Params:
         self.fp32_polish = fp32_polish          # polish preconditioner: the kernel's fp32 sweep inverse
         self.downdate = downdate                # face-adding repairs as downdates of the inverse
         self.dd_max = dd_max                    # ... up to this many added faces per factorization
+        self.dd_rebase = dd_rebase              # ... and any repair that keeps the session's base
+                                                # faces: the added faces re-downdated from the base
         self.hook = hook                        # (studies) dict filled at the first polish session
+        self.trace = trace                      # (studies) list: one event per factorization / repair
+        self.fp32_admm = fp32_admm              # (studies) ADMM inverse in fp32 as the kernel's sweep
+        self.border = border                    # repairs as the kernel's bordered system on the
+                                                # session's base, up to this many columns
+        self.border_extra = border_extra        # ... refinement steps past polish_refine (bordered)
+        self.border_refine = border_refine      # (study) iterative-refinement steps of W = M U
+        self.weak_base = weak_base              # (studies) faces ADMM holds only weakly (gone at
+                                                # this fraction of its dual) enter as downdates
+        self.border_max = border_max            # (studies) repairs as a bordered system on the
+                                                # session's base: up to this many changed faces
 
 
 def project(v, mu, fz_min):
@@ -133,12 +147,18 @@ def solve(inst, p: Params):
 
     def admm_matrix(rho):
         stats['fact'] += 1
+        if p.trace is not None:
+            p.trace.append(('admm', it_now[0], float(rho)))
         Bt = [B[k][:, [3 * l + a for l in range(4) if stance[k, l] for a in range(3)]] for k in range(N)]
         Rt = np.concatenate([np.tile(p.R[[3 * l + a for a in range(3)]], 1) for k in range(N) for l in range(4) if stance[k, l]]) if nf else np.zeros(0, F32)
         H = condense(A, Bt, p.Q, Rt, p.sigma + rho)
+        if p.fp32_admm and nf:
+            return ('M', sweep_inverse32(H))
         return np.linalg.cholesky(H.astype(np.float64)).astype(F32) if nf else None
 
     def solve_L(L, v):
+        if isinstance(L, tuple):
+            return (L[1] @ v.astype(F32)).astype(F32)
         y = np.linalg.solve(L.astype(np.float64), v.astype(np.float64))
         return np.linalg.solve(L.T.astype(np.float64), y).astype(F32)
 
@@ -151,6 +171,8 @@ def solve(inst, p: Params):
         """Reduced basis of the faces in `code` (cmpc_wave.hip polish_setup) and its factorization:
         u = T v + t0; pidx[t] = (px, py, pz) of triple t (-1: no param)."""
         stats['fact'] += 1
+        if p.trace is not None:
+            p.trace.append(('polish', it_now[0]))
         Bt = []; Rt = []; params = []
         t0 = np.zeros(12 * N, F32)
         pidx = np.full((len(tri), 3), -1, int)
@@ -188,6 +210,7 @@ def solve(inst, p: Params):
         if p.fp32_polish or p.downdate:
             # an explicit inverse: fp32 as the kernel's sweep computes it, or float64
             bs['M'] = sweep_inverse32(H) if p.fp32_polish else np.linalg.inv(H.astype(np.float64))
+            bs['M0'] = bs['M']
         else:
             bs['L'] = np.linalg.cholesky(H.astype(np.float64)).astype(F32)
         return bs
@@ -235,10 +258,10 @@ def solve(inst, p: Params):
             prev = step
         return v, step
 
-    def check(bs, v, code, step):
+    def check(bs, v, code, step, u_in=None):
         """KKT check of the faces in `code` at v (forces from the basis, cmpc_wave.hip
         polish_check); returns ok, u, the repaired code, loose."""
-        u = expand(bs, v)
+        u = expand(bs, v) if u_in is None else u_in.astype(F32)
         g, _ = gradient(A, B, d, p.Q, p.R, u.reshape(N, 12))
         g = g.reshape(-1)
         gs = F32(max(np.max(np.abs(g[fidx])), 1e-30))
@@ -324,19 +347,150 @@ def solve(inst, p: Params):
         bs['nadd'] = bs.get('nadd', 0) + len(cons)
         return bs, v
 
+    def border_build(bs, c1):
+        """cmpc_wave.hip border_build: the columns of face set c1 against the base bs (new
+        parameters for dropped base faces, constraints for added faces), W = M U, S^-1."""
+        c0 = bs['code']
+        M = bs['M']
+        ext, cons = [], []
+        for ti, (k, l) in enumerate(tri):
+            a, b = int(c0[ti]), int(c1[ti])
+            px, py, pz = bs['pidx'][ti]
+            sx0 = 1 if a & 2 else (-1 if a & 4 else 0)
+            sy0 = 1 if a & 8 else (-1 if a & 16 else 0)
+            jz = jx = jy = None
+            if (a & 1) and not (b & 1):
+                jz = len(ext); ext.append((ti, 2, np.array([sx0 * p.mu, sy0 * p.mu, 1.0], np.float64)))
+            if sx0 and not (b & a & 6):
+                jx = len(ext); ext.append((ti, 0, np.array([1.0, 0, 0])))
+            if sy0 and not (b & a & 24):
+                jy = len(ext); ext.append((ti, 1, np.array([0, 1.0, 0])))
+            zt = ('v', pz) if not (a & 1) else (('e', jz) if jz is not None else None)
+            zc = float(p.fz_min) if (a & 1) else 0.0
+            if (b & 1) and not (a & 1):
+                cons.append(([('v', pz, 1.0)], float(p.fz_min)))
+            for ax, bits in ((0, (b & 6) & ~(a & 6)), (1, (b & 24) & ~(a & 24))):
+                if not bits:
+                    continue
+                sg = 1.0 if bits & (8 if ax else 2) else -1.0
+                s0 = sy0 if ax else sx0
+                t1 = ('v', py if ax else px) if s0 == 0 else ('e', jy if ax else jx)
+                cz = -sg * float(p.mu) if s0 == 0 else 2.0 * s0 * float(p.mu)
+                terms = [(t1[0], t1[1], 1.0)] + ([(zt[0], zt[1], cz)] if zt is not None else [])
+                cons.append((terms, -cz * zc))
+        k = len(ext) + len(cons)
+        if k > p.border:
+            return None
+        nr = bs['nr']
+        U = np.zeros((nr, k)); D = np.zeros((k, k))
+        Gt = []
+        for j, (ti, ax, dvec) in enumerate(ext):
+            kk, l = tri[ti]
+            u = np.zeros((N, 12), F32); u[kk, 3 * l:3 * l + 3] = dvec
+            g, _ = gradient(A, B, np.zeros_like(d), p.Q, p.R, u)
+            Gt.append(g.reshape(-1).astype(np.float64))
+            U[:, j] = reduce(bs, g.reshape(-1))
+        for i, (ti, ax, dvec) in enumerate(ext):
+            kk, l = tri[ti]
+            for j in range(len(ext)):
+                D[i, j] = dvec @ Gt[j][12 * kk + 3 * l:12 * kk + 3 * l + 3]
+        for c, (terms, rhs) in enumerate(cons):
+            j = len(ext) + c
+            for kind, idx, cf in terms:
+                if kind == 'v':
+                    U[idx, j] += cf
+                else:
+                    D[idx, j] += cf; D[j, idx] += cf
+        Mf = M.astype(np.float64)
+        W = Mf @ U
+        for _ in range(p.border_refine):  # W += M (U - H0 W), H0 applied through the gradient
+            HW = np.zeros_like(W)
+            for j in range(k):
+                ul = expand(bs, W[:, j].astype(F32)) - bs['t0']
+                g, _ = gradient(A, B, np.zeros_like(d), p.Q, p.R, ul.reshape(N, 12))
+                HW[:, j] = reduce(bs, g.reshape(-1)) + p.sigma * W[:, j]
+            W = W + Mf @ (U - HW)
+        S = D - U.T @ W
+        stats['bd_cols'] = stats.get('bd_cols', 0) + k
+        stats['bd_ext'] = stats.get('bd_ext', 0) + len(ext)
+        return dict(ext=ext, cons=cons, W=W, Sinv=np.linalg.inv(S), e=np.zeros(len(ext)), k=k)
+
+    def force_ext(bs, v, bd):
+        u = expand(bs, v).astype(np.float64)
+        if bd is not None:
+            for j, (ti, ax, dvec) in enumerate(bd['ext']):
+                kk, l = tri[ti]
+                u[12 * kk + 3 * l:12 * kk + 3 * l + 3] += bd['e'][j] * dvec
+        return u
+
+    def refine_border(bs, v, bd):
+        """refine() with the bordered Newton step (cmpc_wave.hip border_apply)."""
+        step = np.inf; prev = np.inf
+        M = bs['M'].astype(np.float64)
+        for q in range(p.polish_refine + p.border_extra):
+            stats['refine'] += 1
+            u = force_ext(bs, v, bd)
+            g, _ = gradient(A, B, d, p.Q, p.R, u.astype(F32).reshape(N, 12))
+            g = g.reshape(-1).astype(np.float64)
+            gv = reduce(bs, g.astype(F32)).astype(np.float64)
+            b = []
+            for j, (ti, ax, dvec) in enumerate(bd['ext']):
+                kk, l = tri[ti]
+                b.append(dvec @ g[12 * kk + 3 * l:12 * kk + 3 * l + 3])
+            for terms, rhs in bd['cons']:
+                r = -rhs
+                for kind, idx, cf in terms:
+                    r += cf * (v[idx] if kind == 'v' else bd['e'][idx])
+                b.append(r)
+            z = bd['Sinv'] @ (np.array(b) - bd['W'].T @ gv)
+            dv = M @ gv - bd['W'] @ z
+            ne = len(bd['ext'])
+            v = (v - dv).astype(F32)
+            bd['e'] = bd['e'] - z[:ne]
+            step = max(np.max(np.abs(dv), initial=0), np.max(np.abs(z[:ne]), initial=0))
+            if p.trace is not None:
+                p.trace.append(('bstep', q, float(step), bd['k'], ne))
+            if q + 1 >= p.polish_refine and (step <= p.tol_polish * max(1.0, np.max(np.abs(v), initial=0))
+                                             or step > 0.5 * prev):
+                break
+            prev = step
+        return v, step
+
+    def nchanges(c0, c1):
+        x = np.array(c0) ^ np.array(c1)
+        return int(sum(bin(int(t)).count('1') for t in x))
+
     def session(zv, code, budget, tried):
         """One polish session from ADMM's face set `code`; returns ok, u, the last repaired code
         and the loose flag."""
         if p.hook is not None and 'code' not in p.hook:
             p.hook.update(code=np.array(code).copy(), rho=rho, z=zv.copy())
-        bs = make_basis(code)
-        v = v_from(bs, full(zv).reshape(-1))
+        if p.weak_base > 0 and weak_code[0] is not None:
+            strong = np.array(code) & weak_code[0]
+            bs = make_basis(strong)
+            v = v_from(bs, full(zv).reshape(-1))
+            cons = face_constraints(bs, strong, code)
+            if 0 < len(cons) <= p.dd_max:
+                stats['weak_faces'] = stats.get('weak_faces', 0) + len(cons)
+                bs, v = downdate(bs, v, cons)
+            elif cons:
+                stats['fact'] -= 1
+                bs = make_basis(code)
+                v = v_from(bs, full(zv).reshape(-1))
+        else:
+            bs = make_basis(code)
+            v = v_from(bs, full(zv).reshape(-1))
         rep = 0
         cur_rep[0] = 0
         while True:
-            v, step = refine(bs, v)
-            ok, u, nc, loose = check(bs, v, code, step)
-            if (not ok and bs.get('nadd', 0) > 0 and
+            bd = bs.get('bd')
+            if bd is not None:
+                v, step = refine_border(bs, v, bd)
+                ok, u, nc, loose = check(bs, v, code, step, force_ext(bs, v, bd))
+            else:
+                v, step = refine(bs, v)
+                ok, u, nc, loose = check(bs, v, code, step)
+            if (not ok and (bs.get('nadd', 0) > 0 or (bd is not None and bd['k'] > 0)) and
                     not step <= p.tol_polish * max(1.0, float(np.max(np.abs(u))))):
                 # the downdated preconditioner no longer contracts: refactor the current face set
                 stats['dd_fallback'] += 1
@@ -352,16 +506,46 @@ def solve(inst, p: Params):
             cur_rep[0] = rep
             stats['repairs'] += 1
             drops = np.any((nc & np.array(code)) != np.array(code))
+            if p.trace is not None:
+                co = np.array(code)
+                p.trace.append(('repair', int(np.sum((nc & ~co) != 0)), int(np.sum((co & ~nc) != 0))))
             cons = [] if drops or not p.downdate else face_constraints(bs, code, nc)
-            if p.downdate and not drops and bs.get('nadd', 0) + len(cons) <= p.dd_max:
+            keeps_base = not np.any((nc & bs['code']) != bs['code'])
+            bdn = border_build(bs, nc) if p.border > 0 else None
+            if bdn is not None:
+                stats['dd_repairs'] += 1
+                stats['border_repairs'] = stats.get('border_repairs', 0) + 1
+                bs = dict(bs); bs['bd'] = bdn
+            elif p.border > 0:
+                bs = make_basis(nc)
+                v = v_from(bs, full(zv).reshape(-1))
+            elif p.downdate and not drops and bs.get('nadd', 0) + len(cons) <= p.dd_max:
                 stats['dd_repairs'] += 1
                 bs, v = downdate(bs, v, cons)
+            elif p.border_max > 0 and nchanges(bs['code'], nc) <= p.border_max:
+                # (study) the bordered Schur system of the base inverse: the repaired set's exact
+                # inverse without a factorization (one symv per changed face)
+                stats['border_repairs'] = stats.get('border_repairs', 0) + 1
+                b0 = bs['code']
+                bs = make_basis(nc)
+                stats['fact'] -= 1
+                bs['code'] = b0
+                v = v_from(bs, u)
+            elif p.downdate and p.dd_rebase and keeps_base and \
+                    len(face_constraints(bs, bs['code'], nc)) <= p.dd_max:
+                # a drop of added faces only: the session's base inverse, downdated afresh
+                stats['dd_repairs'] += 1
+                stats['dd_rebases'] = stats.get('dd_rebases', 0) + 1
+                base = dict(bs); base['M'] = bs['M0']; base['nadd'] = 0
+                bs, v = downdate(base, v, face_constraints(bs, bs['code'], nc))
             else:
                 bs = make_basis(nc)
                 v = v_from(bs, full(zv).reshape(-1))
             code = nc
 
     cur_rep = [0]  # repairs made so far in the current session (repair_top_rep)
+    it_now = [0]   # (studies) the ADMM iteration, for the trace
+    weak_code = [None]  # (studies) the face set at a fraction of ADMM's dual (weak_base)
 
     failed_starts = []
     # the NC >= 128 bins (nf > 96) start from rho / 2 and return to rho after their first
@@ -376,6 +560,7 @@ def solve(inst, p: Params):
     prev_code = None; stable = 0; last_pol = 0
     status = -2; it = 0; U = None
     for it in range(1, p.max_iter + 1):
+        it_now[0] = it
         g, _ = gradient(A, B, d, p.Q, p.R, full(x))
         g = g.reshape(-1)[fidx]
         rhs = F32(rho) * (z - x) - g - y
@@ -397,6 +582,9 @@ def solve(inst, p: Params):
             # a session: polish ADMM's face set, then repair it.  A set that started a failed
             # session before is polished once more without repairs; a repair that returns to a
             # set this session already tried ends the session (cmpc_wave.hip kFailMem/kTryMem).
+            if p.weak_base > 0:
+                _, weak_code[0] = project((xr + F32(1 - p.weak_base) * y / F32(rho)).reshape(-1, 3),
+                                          p.mu, p.fz_min)
             start = code.tobytes()
             seen = start in failed_starts[-4:]
             tried = [start]
@@ -419,6 +607,8 @@ def solve(inst, p: Params):
                 rho_low = False; rho = p.rho; L = admm_matrix(rho)
             elif not parked:
                 stats['fact'] += 1  # the polish inverse replaced the ADMM one: refactor
+                if p.trace is not None:
+                    p.trace.append(('admm-restore', it, float(rho)))
         if p.adaptive_interval and it % p.adaptive_interval == 0:
             rp = np.max(np.abs(x - z)); rd = np.max(np.abs(g + y))
             npn = max(np.max(np.abs(x)), np.max(np.abs(z)), 1e-30)

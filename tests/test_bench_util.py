@@ -18,7 +18,7 @@ def test_counters_lookup_ignores_template_flag():
     for c in (new, old):
         assert bench._counters_of(c, "solve_group_kernel<128, 96>") is rec_a
         assert bench._counters_of(c, "solve_group_kernel<192, 160>") is rec_b
-        assert bench._counters_of(c, "solve_team_kernel<4>") is None
+        assert bench._counters_of(c, "solve_team_kernel<4, 1>") is None
     assert bench._counters_of(None, "solve_group_kernel<128, 96>") is None
 
 

@@ -63,3 +63,27 @@ def test_algorithm_model_face_downdates():
         facts[0] += base["fact"]
         facts[1] += out["fact"]
     assert dd_reps > 0 and facts[1] < facts[0], (dd_reps, facts)
+
+
+def test_algorithm_model_bordered_repairs():
+    """tests/algo_spec.py with the kernel's bordered repairs (cmpc_wave.hip border_build /
+    border_apply: dropped base faces as new parameters, added faces as constraints, on the
+    session's base inverse): the same certified optima on the hard fixture instances, with
+    repairs that drop faces and no more factorizations than the downdates alone."""
+    import algo_spec
+    from parity_util import load_fixture, fixture_batch, rel_err_U
+    fx = load_fixture("qp_hard.npz")
+    fb = fixture_batch(fx)
+    facts = [0, 0]
+    borders = 0
+    for i in range(len(fx["w"])):
+        inst = {k: v[i] for k, v in fb.items()}
+        dd = algo_spec.solve(inst, algo_spec.Params(fp32_polish=True, downdate=True, dd_max=6))
+        out = algo_spec.solve(inst, algo_spec.Params(fp32_polish=True, border=5, border_extra=12))
+        assert out["status"] == 1
+        w = np.concatenate([np.zeros(192), out["U"].reshape(-1)])
+        assert rel_err_U(w[None], fx["w"][i:i + 1])[0] < 1e-4
+        borders += out.get("border_repairs", 0)
+        facts[0] += dd["fact"]
+        facts[1] += out["fact"]
+    assert borders > 0 and facts[1] <= facts[0], (borders, facts)
