@@ -203,6 +203,16 @@ struct Cfg {
 //  * the starting sets of the last kFailMem failed sessions are remembered; ADMM's face set can
 //    stay "stable" while still wrong, and a session that starts from a remembered set polishes
 //    it once more (it may pass now, from ADMM's better iterate) but makes no repairs.
+// (Knob, off.)  The NC <= 128 bins would start a polish session after polish_stable -
+// CMPC_LIGHT_STABLE_DELTA unchanged ADMM iterations.  With 1, A/B in one gpurun call, two
+// alternations (round 4): config 3 at 65,536 8.65 -> 8.42 ms, config 2 unchanged, config 1 at
+// 256 0.193 -> 0.189 ms, the N = 8 shard rehearsal 1.88 -> 1.81 ms; but it moves which
+// next-tick instance lands on the fp32 KKT check's flat-direction limit, and
+// test_warm_next_tick's warm result 3485 ends 2.11e-4 from the optimum (the test allows 2e-4).
+// Not on until the check can certify those directions.
+#ifndef CMPC_LIGHT_STABLE_DELTA
+#define CMPC_LIGHT_STABLE_DELTA 0
+#endif
 #ifndef CMPC_REFINE_N  // diagnostic override of the refinement count
 #define CMPC_REFINE_N P.polish_refine
 #endif
@@ -2630,8 +2640,13 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     bool do_pol = false;
     // back off before a further attempt, longer after failed sessions: both the stable run and
     // the distance to the last session grow as polish_stable x 2^min(nfail, kBackoffCap)
-    const int backoff = P.polish_stable << min(nfail, kBackoffCap);
-    int need = P.polish_stable;  // (kStableGrow: the stable run required grows per failed session)
+#if CMPC_LIGHT_STABLE_DELTA > 0
+    const int pstable = max(1, P.polish_stable - (NC <= 128 ? CMPC_LIGHT_STABLE_DELTA : 0));
+#else
+    const int pstable = P.polish_stable;
+#endif
+    const int backoff = pstable << min(nfail, kBackoffCap);
+    int need = pstable;  // (kStableGrow: the stable run required grows per failed session)
     for (int f = 0; f < min(nfail, kBackoffCap); ++f) need *= kStableGrow;
     if (stable >= need && !last && it - last_pol >= backoff &&
         (P.check_every == 1 || it % P.check_every == 0)) {  // (OPTS check_termination)

@@ -19,7 +19,7 @@ class Params:
                  repair_top_from=1, repair_top_rep=2, repair_frac=0.5, stable_grow=3,
                  fp32_polish=False, downdate=False, dd_max=24, dd_rebase=False, hook=None,
                  trace=None, fp32_admm=False, border_max=0, weak_base=0.0, border=0,
-                 border_extra=4, border_refine=0):
+                 border_extra=4, border_refine=0, light_stable_delta=0):
         self.N = N
         self.Q = np.array([1, 1, 50, 10, 20, 1, 2, 2, 1, 1, 1, 1], F32) if Q is None else np.asarray(Q, F32)
         self.R = np.full(12, 1e-5, F32) if R is None else np.asarray(R, F32)
@@ -48,6 +48,8 @@ class Params:
                                                 # session's base, up to this many columns
         self.border_extra = border_extra        # ... refinement steps past polish_refine (bordered)
         self.border_refine = border_refine      # (study) iterative-refinement steps of W = M U
+        self.light_stable_delta = light_stable_delta  # NC <= 128: polish after stable_checks - this
+                                                      # (cmpc_wave.hip CMPC_LIGHT_STABLE_DELTA, off)
         self.weak_base = weak_base              # (studies) faces ADMM holds only weakly (gone at
                                                 # this fraction of its dual) enter as downdates
         self.border_max = border_max            # (studies) repairs as a bordered system on the
@@ -550,6 +552,8 @@ def solve(inst, p: Params):
     failed_starts = []
     # the NC >= 128 bins (nf > 96) start from rho / 2 and return to rho after their first
     # failed polish session (cmpc_wave.hip solve_instance, rho_low)
+    # the NC <= 128 bins polish one stable iteration earlier (cmpc_wave.hip CMPC_LIGHT_STABLE_DELTA)
+    pstable = max(1, p.stable_checks - (p.light_stable_delta if nf <= 128 else 0))
     rho_low = nf > 96
     rho = p.rho * (0.5 if rho_low else 1.0)
     L = admm_matrix(rho)
@@ -576,8 +580,8 @@ def solve(inst, p: Params):
         else:
             stable = 0
         prev_code = code
-        backoff = p.stable_checks << min(len(failed_starts), p.backoff_cap)   # cmpc_wave.hip kBackoffCap
-        if stable >= p.stable_checks * p.stable_grow ** min(len(failed_starts), p.backoff_cap) and it - last_pol >= backoff:
+        backoff = pstable << min(len(failed_starts), p.backoff_cap)   # cmpc_wave.hip kBackoffCap
+        if stable >= pstable * p.stable_grow ** min(len(failed_starts), p.backoff_cap) and it - last_pol >= backoff:
             last_pol = it
             # a session: polish ADMM's face set, then repair it.  A set that started a failed
             # session before is polished once more without repairs; a repair that returns to a
