@@ -135,8 +135,6 @@ def parse(argv=None):
                     help="SolverParams override key=value (experiments; also $CMPC_PARAMS k=v,k=v)")
     ap.add_argument("--team", type=int, default=-1,
                     help="small-batch team mode for B <= this (cmpc_plan_set_team): -1 auto, 0 off")
-    ap.add_argument("--ipm", type=int, default=int(os.environ.get("CMPC_IPM_BATCH", "-1")),
-                    help="interior-point fallback kernels for B <= this (cmpc_plan_set_ipm): -1 auto")
     ap.add_argument("--heavy-first", type=int, default=int(os.environ.get("CMPC_HEAVY_FIRST", "-1")),
                     help="NC >= 160 class first for B >= this (cmpc_plan_set_heavy_first): -1 auto, 0 never")
     ap.add_argument("--lib", type=str, default=None,
@@ -210,7 +208,7 @@ def timed_steps(step, steps, warmup, sync, barrier, reduce_max):
 def _counters_of(counters, name):
     """PMC record of kernel `name` in profiles/*_counters.json (keys are rocprof's demangled
     names, e.g. 'void cmpc::solve_group_kernel<128, 96>')."""
-    def norm(n):  # the IPM template flag (<.., .., false>) is not part of the bench's label
+    def norm(n):  # (round-4 records name the kernels with a third template flag, <.., .., false>)
         return re.sub(r",(true|false)>", ">", n.replace(" ", ""))
     for k, v in (counters or {}).items():
         if isinstance(v, dict) and norm(k).endswith(norm(name)):
@@ -374,8 +372,6 @@ def main(argv=None):
     plan = Plan(SolverParams(max_batch=max_b, **over), device=dev)
     if args.team != -1 and hasattr(plan.lib, "cmpc_plan_set_team"):
         plan.set_team(args.team)
-    if args.ipm != -1 and hasattr(plan.lib, "cmpc_plan_set_ipm"):
-        plan.set_ipm(args.ipm)
     if args.heavy_first != -1 and hasattr(plan.lib, "cmpc_plan_set_heavy_first"):
         plan.set_heavy_first(args.heavy_first)
     stream = torch.cuda.current_stream(dev)

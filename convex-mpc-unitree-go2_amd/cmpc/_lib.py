@@ -12,8 +12,10 @@ from pathlib import Path
 
 from .build import LIB
 
-ABI_VERSION = 4
-ABI_COMPAT = (3, 4)   # cmpc_params layouts identical to this one (A/B builds of earlier rounds)
+ABI_VERSION = 5
+# ABI 4 (round 4) has this cmpc_params layout, bins and solve kernels (its reserved0 was
+# ipm_facts, 0 by default): its builds load only for A/B experiments, with CMPC_ALLOW_ABI4=1
+ABI_COMPAT = (4, 5) if os.environ.get("CMPC_ALLOW_ABI4") == "1" else (5,)
 CMPC_OK = 0
 
 
@@ -36,7 +38,7 @@ class CParams(ctypes.Structure):
         ("polish_refine", ctypes.c_int32),
         ("polish_tol", ctypes.c_float),
         ("polish_repairs", ctypes.c_int32),
-        ("ipm_facts", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
         ("check_termination", ctypes.c_int32),
         ("max_batch", ctypes.c_int64),
     ]
@@ -45,7 +47,7 @@ class CParams(ctypes.Structure):
 EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_destroy",
            "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_plan_set_team", "cmpc_plan_team_batch",
-           "cmpc_plan_set_ipm", "cmpc_plan_ipm_batch", "cmpc_plan_set_heavy_first",
+           "cmpc_plan_set_heavy_first",
            "cmpc_plan_heavy_first_batch", "cmpc_plan_solve_kernel", "cmpc_last_error",
            "cmpc_version")
 NUM_BINS = 5
@@ -61,8 +63,8 @@ _lib = None
 
 
 def load(path: str | Path | None = None) -> ctypes.CDLL:
-    """Load libcmpc.so (in-tree; $CMPC_LIB names a variant build, e.g. the one with the
-    interior-point fallback) and declare the prototypes.  Raises if it is missing."""
+    """Load libcmpc.so (in-tree; $CMPC_LIB names a variant build, e.g. a diagnostic one) and
+    declare the prototypes.  Raises if it is missing."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -111,11 +113,6 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
         lib.cmpc_plan_set_team.restype = ctypes.c_int
         lib.cmpc_plan_team_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         lib.cmpc_plan_team_batch.restype = ctypes.c_int
-    if hasattr(lib, "cmpc_plan_set_ipm"):
-        lib.cmpc_plan_set_ipm.argtypes = [vp, ctypes.c_int64]
-        lib.cmpc_plan_set_ipm.restype = ctypes.c_int
-        lib.cmpc_plan_ipm_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
-        lib.cmpc_plan_ipm_batch.restype = ctypes.c_int
     if hasattr(lib, "cmpc_plan_set_heavy_first"):
         lib.cmpc_plan_set_heavy_first.argtypes = [vp, ctypes.c_int64]
         lib.cmpc_plan_set_heavy_first.restype = ctypes.c_int

@@ -39,7 +39,6 @@ class SolverParams:
     polish_refine: int = 4
     polish_tol: float = 1e-5
     polish_repairs: int = 6
-    ipm_facts: int = 0
     check_termination: int = 1   # OPTS check_termination (reference: 10; include/cmpc.h)
     max_batch: int = 65536
 
@@ -98,8 +97,12 @@ class Plan:
             cp = self.params.to_c()
             d = _lib.CParams()
             self.lib.cmpc_params_default(ctypes.byref(d))
-            if d.abi_version in _lib.ABI_COMPAT:  # (an earlier round's A/B build, same layout)
-                cp.abi_version = d.abi_version
+            if d.abi_version != _lib.ABI_VERSION:
+                if d.abi_version not in _lib.ABI_COMPAT:
+                    raise CmpcError(f"cmpc: library ABI {d.abi_version}, this binding is ABI "
+                                    f"{_lib.ABI_VERSION} (an ABI-4 A/B build loads with "
+                                    f"CMPC_ALLOW_ABI4=1)")
+                cp.abi_version = d.abi_version   # (A/B experiments only: same layout and kernels)
             _check(self.lib, self.lib.cmpc_plan_create(ctypes.byref(cp), ctypes.byref(h)),
                    "cmpc_plan_create")
         self._h = h
@@ -136,19 +139,6 @@ class Plan:
         v = ctypes.c_int64()
         _check(self.lib, self.lib.cmpc_plan_team_batch(self._h, ctypes.byref(v)),
                "cmpc_plan_team_batch")
-        return int(v.value)
-
-    def set_ipm(self, max_batch: int):
-        """Kernel variants with the interior-point fallback for solves of B <= max_batch (above
-        the team bound): -1 = automatic (B <= 64 x CUs, the default), 0 = never
-        (cmpc_plan_set_ipm)."""
-        _check(self.lib, self.lib.cmpc_plan_set_ipm(self._h, int(max_batch)), "cmpc_plan_set_ipm")
-
-    def ipm_batch(self) -> int:
-        """The largest batch solved by the fallback-carrying kernels (cmpc_plan_ipm_batch)."""
-        v = ctypes.c_int64()
-        _check(self.lib, self.lib.cmpc_plan_ipm_batch(self._h, ctypes.byref(v)),
-               "cmpc_plan_ipm_batch")
         return int(v.value)
 
     def set_heavy_first(self, min_batch: int):

@@ -196,6 +196,17 @@ CONFIGS = {
 }
 
 
+def next_tick(batch: dict, seed: int = 5) -> dict:
+    """The next MPC tick's problem in the warm-start proxy (tests, bench, certify_sample): the
+    state x0 moves by N(0, 2e-3) on position / attitude and N(0, 2e-2) on the velocities; the
+    reference, gait and dynamics stay (centroidal_mpc.py:91-95 warm-starts such a tick from the
+    previous solution)."""
+    rng = np.random.default_rng(seed)
+    out = dict(batch)
+    out["x0"] = batch["x0"] + rng.normal(scale=[2e-3] * 6 + [2e-2] * 6, size=batch["x0"].shape)
+    return out
+
+
 def make_config(cfg: int, B: int | None = None):
     if cfg == 3:
         Bt = 65536 if B is None else B

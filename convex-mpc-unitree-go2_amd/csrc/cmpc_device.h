@@ -19,7 +19,6 @@ struct KParams {
   int polish_stable;
   int polish_refine;
   int polish_repairs;
-  int ipm_facts;        // interior-point fallback after this many factorizations (0: never)
   int check_every;      // termination (polish trigger) test every this many ADMM iterations
   int latency_mode;  // set per launch: at most one wave per SIMD (small batch), see condense_tiles
 };

@@ -39,9 +39,6 @@ struct cmpc_plan {
   int team_grid1 = 0;   // at one per CU (<W, 1>: B <= CUs)
   size_t team_slab = 0;
   int64_t team_max_batch = -1;  // -1: automatic (B <= 4 x CUs: at most one wave per SIMD)
-  // tail-bound batches (B <= ipm_max_batch): the one-wave kernel variants with the
-  // interior-point fallback for hard instances
-  int64_t ipm_max_batch = -1;   // -1: automatic (B <= 64 x CUs)
   // batches of B >= heavy_first_min_batch submit the NC >= 160 class first
   int64_t heavy_first_min_batch = -1;  // -1: automatic (B > 16 x CUs), 0: never
   // The solve kernels (cmpc_wave.hip solve_group_kernel: the NC <= 128 class, the NC 144 / 160
@@ -94,37 +91,19 @@ int group_first_bin(int k) { return k == 0 ? 1 : (k == 1 ? 3 : 4); }
 
 constexpr int kTeamWaves = 4;
 
-// The kernel variants carrying the interior-point fallback are compiled only with
-// -DCMPC_WITH_IPM (scripts/build_variant.sh ipm -DCMPC_WITH_IPM): no measured batch gains from
-// them since the damped repairs, and the default library keeps only the kernels that run.
-#ifdef CMPC_WITH_IPM
-constexpr bool kHasIpm = true;
-#else
-constexpr bool kHasIpm = false;
-#endif
-
-KernelFn group_fn(int k, bool ipm = false) {
-#ifdef CMPC_WITH_IPM
-  if (ipm)
-    return k == 0 ? cmpc::solve_group_kernel<128, 96, true>
-                  : (k == 1 ? cmpc::solve_group_kernel<160, 144, true> : cmpc::solve_group_kernel<192, 0, true>);
-#else
-  (void)ipm;
-#endif
-  return k == 0 ? cmpc::solve_group_kernel<128, 96, false>
-                : (k == 1 ? cmpc::solve_group_kernel<160, 144, false> : cmpc::solve_group_kernel<192, 0, false>);
+KernelFn group_fn(int k) {
+  return k == 0 ? cmpc::solve_group_kernel<128, 96>
+                : (k == 1 ? cmpc::solve_group_kernel<160, 144> : cmpc::solve_group_kernel<192, 0>);
 }
 
-const char* group_name(int k, bool ipm) {
-  static const char* names[2][kNumGroups] = {
-      {"solve_group_kernel<128, 96, false>", "solve_group_kernel<160, 144, false>",
-       "solve_group_kernel<192, 0, false>"},
-      {"solve_group_kernel<128, 96, true>", "solve_group_kernel<160, 144, true>",
-       "solve_group_kernel<192, 0, true>"}};
-  return names[ipm ? 1 : 0][k];
+const char* group_name(int k) {
+  static const char* names[kNumGroups] = {"solve_group_kernel<128, 96>",
+                                          "solve_group_kernel<160, 144>",
+                                          "solve_group_kernel<192, 0>"};
+  return names[k];
 }
 
-// park slab per wave (floats): the one-wave inverse (+ the interior-point state)
+// park slab per wave (floats): the one-wave inverse
 size_t group_slab(int k) {
   return k == 0 ? std::max(cmpc::Cfg<128>::SLAB, cmpc::Cfg<96>::SLAB)
                 : (k == 1 ? std::max(cmpc::Cfg<160>::SLAB, cmpc::Cfg<144>::SLAB) : cmpc::Cfg<192>::SLAB);
@@ -163,7 +142,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->polish_refine = 4;
   p->polish_tol = 1e-5f;
   p->polish_repairs = 6;
-  p->ipm_facts = 0;  // opt-in since the damped repairs
+  p->reserved0 = 0;
   p->check_termination = 1;  // (reference OPTS: 10, accepted; see include/cmpc.h)
   p->max_batch = 65536;
 }
@@ -186,13 +165,13 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   if (!(p->rho > 0.f) || !(p->sigma >= 0.f) || !(p->alpha > 0.f && p->alpha < 2.f))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: need rho > 0, sigma >= 0, 0 < alpha < 2");
   if (p->polish_stable < 1 || p->polish_refine < 1 || !(p->polish_tol > 0.f) ||
-      p->polish_repairs < 0 || p->ipm_facts < 0 || p->check_termination < 1)
+      p->polish_repairs < 0 || p->check_termination < 1)
     return fail(CMPC_E_INVALID, "cmpc_plan_create: polish settings out of range");
   if (p->adaptive_rho_interval < 0 || p->max_batch < 1 || p->max_batch > (1LL << 30))
     return fail(CMPC_E_INVALID, "cmpc_plan_create: adaptive_rho_interval/max_batch out of range");
-  if (!kHasIpm && p->ipm_facts > 0)
-    return fail(CMPC_E_INVALID, "cmpc_plan_create: ipm_facts > 0 needs a library built with "
-                                "-DCMPC_WITH_IPM (the interior-point fallback is not in this build)");
+  if (p->reserved0 != 0)
+    return fail(CMPC_E_INVALID, "cmpc_plan_create: reserved0 must be 0 (ABI 4's ipm_facts: the "
+                                "interior-point fallback was removed)");
 
   cmpc_plan* pl = new cmpc_plan();
   pl->p = *p;
@@ -215,7 +194,6 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   k.polish_stable = p->polish_stable;
   k.polish_refine = p->polish_refine;
   k.polish_repairs = p->polish_repairs;
-  k.ipm_facts = p->ipm_facts;
   k.check_every = p->check_termination;
 
   hipError_t e = hipGetDevice(&pl->device);
@@ -224,17 +202,12 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, pl->device);
   pl->cus = cus;
   if (e != hipSuccess) { delete pl; return hip_fail(e, "hipDeviceGetAttribute"); }
-  // persistent grids: resident workgroups per CU x CUs, the smaller of the kernel variants
-  // without and with the interior-point fallback (both are launched with the same grid)
+  // persistent grids: resident workgroups per CU x CUs
   size_t work_floats = 0;
   for (int k = 0; k < kNumGroups; ++k) {
-    int nb = 1 << 30;
-    for (int v = 0; v < (kHasIpm ? 2 : 1); ++v) {
-      int b = 0;
-      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, group_fn(k, v == 1), 64, 0);
-      if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
-      nb = std::min(nb, b);
-    }
+    int nb = 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, group_fn(k), 64, 0);
+    if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
     if (nb < 1) { delete pl; return fail(CMPC_E_HIP, "cmpc_plan_create: solve kernel cannot be resident"); }
 #ifdef CMPC_STAMPS
     if (const char* cap = getenv("CMPC_BLOCKS_PER_CU")) {  // diagnostic build: occupancy sweep
@@ -257,7 +230,9 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, cmpc::solve_team_kernel<kTeamWaves, 1>,
                                                      64 * kTeamWaves, 0);
     if (e != hipSuccess) { delete pl; return hip_fail(e, "hipOccupancyMaxActiveBlocksPerMultiprocessor"); }
-    pl->team_grid1 = nb < 1 ? 1 : nb > 1 ? cus : nb * cus;
+    // (0 if the one-per-CU image cannot be resident: team_one_per_cu then never selects it and
+    // the two-per-CU image serves every team batch)
+    pl->team_grid1 = nb < 1 ? 0 : cus;
     pl->team_slab = std::max({cmpc::TeamCfg<192, kTeamWaves>::SLAB, cmpc::TeamCfg<160, kTeamWaves>::SLAB,
                               cmpc::TeamCfg<128, kTeamWaves>::SLAB, cmpc::TeamCfg<96, kTeamWaves>::SLAB});
     work_floats = std::max(work_floats, (size_t)pl->team_grid * pl->team_slab);
@@ -334,13 +309,8 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
                     cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
 }
 
-static int64_t ipm_batch(const cmpc_plan* pl) {
-  return pl->ipm_max_batch >= 0 ? pl->ipm_max_batch : 64LL * pl->cus;
-}
-
 static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParams& kp,
-                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g,
-                         bool ipm) {
+                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
   hipError_t e;
   cmpc_plan::Rec rec{nullptr, nullptr, k};
   const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
@@ -356,7 +326,7 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
     if ((e = hipEventRecord(rec.a, s)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   const int qa = group_first_bin(k);
-  hipLaunchKernelGGL(group_fn(k, ipm), dim3(g), dim3(64), 0, s, kp, in, out,
+  hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
                      pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
@@ -387,7 +357,9 @@ static bool team_one_per_cu(const cmpc_plan* pl, int64_t B) {
     const char* v = getenv("CMPC_TEAM_OCC");
     return v ? atoi(v) : 0;
   }();
-  return occ != 2 && B <= pl->team_grid1;
+  // (experiment knob CMPC_TEAM_OCC: 2 = always the two-per-CU image, 1 = always one per CU,
+  // persistent over B / CUs instances per workgroup)
+  return occ != 2 && pl->team_grid1 > 0 && (occ == 1 || B <= pl->team_grid1);
 }
 
 // team mode: one launch for every bin; timed as solve kernel 0 (kernel 1 records no call)
@@ -437,8 +409,6 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   cmpc::KParams kp = pl->kp;
   // at most one wave per SIMD: latency-bound, the condensation with fewer MFMAs wins
   kp.latency_mode = (B <= 4LL * pl->cus) ? 1 : 0;
-  // tail-bound batch: the kernel variants with the interior-point fallback
-  const bool ipm = kHasIpm && pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
   if (B <= 1024) {  // one workgroup bins the batch and zeroes the queue heads (no memset)
     hipLaunchKernelGGL(cmpc::bin_small_kernel, dim3(1), dim3(1024), 0, st, pl->kp.N, (int)B,
                        in.contact, pl->d_counters, pl->d_counters + cmpc::kNumBins, pl->d_lists,
@@ -486,16 +456,20 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   }
   unsigned gk[kNumGroups];
   for (int k = 0; k < kNumGroups; ++k) gk[k] = (unsigned)(pl->grid[k] < B ? pl->grid[k] : B);
+  {  // (experiment knob CMPC_TOP_GRID: cap the NC 192 kernel's persistent grid)
+    static const int cap = [] { const char* v = getenv("CMPC_TOP_GRID"); return v ? atoi(v) : 0; }();
+    if (cap > 0 && gk[2] > (unsigned)cap) gk[2] = (unsigned)cap;
+  }
   if (top) {
-    rc = record_launch(pl, 2, pl->top, kp, in, out, gk[2], ipm);
+    rc = record_launch(pl, 2, pl->top, kp, in, out, gk[2]);
     if (rc != CMPC_OK) return rc;
   }
   const int64_t hmin = heavy_first_batch(pl);
   const int first = (big && hmin > 0 && B >= hmin) ? 1 : 0;  // class submitted first
-  rc = record_launch(pl, first, st, kp, in, out, gk[first], ipm);
+  rc = record_launch(pl, first, st, kp, in, out, gk[first]);
   if (rc != CMPC_OK) return rc;
   if (big) {
-    rc = record_launch(pl, 1 - first, pl->side, kp, in, out, gk[1 - first], ipm);
+    rc = record_launch(pl, 1 - first, pl->side, kp, in, out, gk[1 - first]);
     if (rc != CMPC_OK) return rc;
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
@@ -624,19 +598,6 @@ int cmpc_plan_team_batch(const cmpc_plan* pl, int64_t* max_batch) {
   return CMPC_OK;
 }
 
-int cmpc_plan_set_ipm(cmpc_plan* pl, int64_t max_batch) {
-  if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_ipm: null plan");
-  if (max_batch < -1) return fail(CMPC_E_INVALID, "cmpc_plan_set_ipm: max_batch must be >= -1");
-  pl->ipm_max_batch = max_batch;
-  return CMPC_OK;
-}
-
-int cmpc_plan_ipm_batch(const cmpc_plan* pl, int64_t* max_batch) {
-  if (!pl || !max_batch) return fail(CMPC_E_INVALID, "cmpc_plan_ipm_batch: null argument");
-  *max_batch = ipm_batch(pl);
-  return CMPC_OK;
-}
-
 int cmpc_plan_set_heavy_first(cmpc_plan* pl, int64_t min_batch) {
   if (!pl) return fail(CMPC_E_INVALID, "cmpc_plan_set_heavy_first: null plan");
   if (min_batch < -1) return fail(CMPC_E_INVALID, "cmpc_plan_set_heavy_first: min_batch must be >= -1");
@@ -654,9 +615,8 @@ const char* cmpc_plan_solve_kernel(const cmpc_plan* pl, int64_t B, int k) {
   if (!pl || B < 1 || k < 0 || k >= kNumGroups) return nullptr;
   if (B <= team_batch(pl))
     return k != 0 ? nullptr : team_one_per_cu(pl, B) ? "solve_team_kernel<4, 1>" : "solve_team_kernel<4, 2>";
-  const bool ipm = kHasIpm && pl->kp.ipm_facts > 0 && B <= ipm_batch(pl);
   if (!has_group(pl, k)) return nullptr;
-  return group_name(k, ipm);
+  return group_name(k);
 }
 
 int cmpc_plan_timing_read(cmpc_plan* pl, float* ms_per_kernel, int32_t* calls_per_kernel) {

@@ -28,9 +28,13 @@
  *   w_out   [B][24N]           fp32   reference decision layout (centroidal_mpc.py:44,
  *                                      test_MPC.py:190-192): w = [x_1..x_N | u_0..u_{N-1}],
  *                                      each 12 contiguous, i.e. vec(X (12,N),'F') then vec(U,'F')
- *   status  [B]                int32  1 solved (KKT-verified active-set polish),
- *                                     2 solved inaccurate (ADMM residuals within eps, polish not
- *                                       verified), -2 max iterations, -10 numerical failure
+ *   status  [B]                int32  1 solved (KKT-verified active-set polish: primal
+ *                                       feasibility, converged refinement, and every held face's
+ *                                       multiplier within a bound that limits the force error
+ *                                       its release could cause),
+ *                                     2 solved inaccurate (ADMM residuals within eps, or a polish
+ *                                       accepted loosely without that bound), -2 max iterations,
+ *                                     -10 numerical failure
  *   iters   [B]                int32  ADMM iterations taken
  *
  * Threading: one plan per host thread / stream.  cmpc_solve is asynchronous on `stream`
@@ -47,8 +51,10 @@
 extern "C" {
 #endif
 
-/* 4: three solve-kernel timing slots (CMPC_NUM_SOLVE_KERNELS); cmpc_params is unchanged from 3 */
-#define CMPC_ABI_VERSION 4
+/* 5: the interior-point variant and its cmpc_plan_set_ipm / cmpc_plan_ipm_batch are gone
+ *    (cmpc_params.reserved0 must be 0); status 1 is KKT-verified with face multipliers bounded
+ *    in force units.  4: three solve-kernel timing slots. */
+#define CMPC_ABI_VERSION 5
 
 #define CMPC_OK 0
 #define CMPC_E_INVALID (-22)   /* bad argument / parameter (EINVAL) */
@@ -78,14 +84,8 @@ typedef struct cmpc_params {
   float polish_tol;       /* relative KKT tolerance for accepting the polished point */
   int32_t polish_repairs; /* active-set repairs (add violated / drop negative-multiplier faces
                              and re-polish) before resuming ADMM */
-  int32_t ipm_facts;      /* EXPERIMENTAL, variant builds only (-DCMPC_WITH_IPM): an instance that
-                             has failed a polish session and spent this many factorizations
-                             identifies its face set by interior-point steps (hard instances,
-                             DESIGN.md 4h); 0 = never.  Default 0: with the damped repairs the
-                             variants without the fallback are faster on every measured batch
-                             (config 3 at 8,192 2.86 -> 2.25 ms).  The default library does
-                             not carry those kernels: cmpc_plan_create rejects ipm_facts > 0
-                             (CMPC_E_INVALID) there */
+  int32_t reserved0;      /* must be 0 (ABI 4's ipm_facts: the interior-point fallback was
+                             removed in ABI 5) */
   int32_t check_termination; /* ADMM iterations between termination tests (OPTS check_termination,
                              centroidal_mpc.py:31): the polish trigger (face set stable for
                              polish_stable iterations -> active-set polish + KKT check, the only
@@ -249,12 +249,11 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
  * kernel k (0, 1 or 2) of a batch of B instances, or returns NULL if that slot is not launched:
  *   B <= cmpc_plan_team_batch:  "solve_team_kernel<4, 1>" (B <= CUs: one workgroup per CU)
  *                               or "solve_team_kernel<4, 2>" (k = 0 only);
- *   larger batches:             "solve_group_kernel<128, 96, IPM>" (k = 0, the NC <= 128
- *                               class), "solve_group_kernel<160, 144, IPM>" (k = 1, the
+ *   larger batches:             "solve_group_kernel<128, 96>" (k = 0, the NC <= 128
+ *                               class), "solve_group_kernel<160, 144>" (k = 1, the
  *                               NC 144 / 160 class; NULL if N is too short to need it) and
- *                               "solve_group_kernel<192, 0, IPM>" (k = 2, the NC 192 bin, more
- *                               than 160 free forces; NULL if N is too short); IPM = true for
- *                               B <= cmpc_plan_ipm_batch in -DCMPC_WITH_IPM builds.  Slots are
+ *                               "solve_group_kernel<192, 0>" (k = 2, the NC 192 bin, more
+ *                               than 160 free forces; NULL if N is too short).  Slots are
  *                               per kernel, whichever class is submitted first
  *                               (cmpc_plan_set_heavy_first).
  * While enabled, cmpc_solve records a hipEvent pair around each solve-kernel launch on the
@@ -275,15 +274,6 @@ const char* cmpc_plan_solve_kernel(const cmpc_plan* plan, int64_t B, int k);
  * it for B <= 4 x CUs; 0 disables it.  cmpc_plan_team_batch returns the effective bound. */
 int cmpc_plan_set_team(cmpc_plan* plan, int64_t max_batch);
 int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
-
-/* Tail-bound batches (variant builds with -DCMPC_WITH_IPM).  When cmpc_params.ipm_facts > 0, a batch of B <= max_batch
- * instances (one wave per QP, i.e. above the small-batch bound) runs the kernel variants that
- * carry the interior-point fallback for hard instances: a small batch or an N-GPU
- * shard takes as long as its slowest instance.  Large batches run the variants without it (its
- * code costs registers on the hot path).  max_batch = -1 (the default) selects B <= 64 x CUs;
- * 0 never.  cmpc_plan_ipm_batch returns the effective bound. */
-int cmpc_plan_set_ipm(cmpc_plan* plan, int64_t max_batch);
-int cmpc_plan_ipm_batch(const cmpc_plan* plan, int64_t* max_batch);
 
 /* Launch order of the two register classes.  A batch above the small-batch bound launches one
  * persistent kernel per register class (NC <= 128: two waves per SIMD; NC 144 / 160: one; plus

@@ -1,8 +1,7 @@
 #!/bin/bash
 # Build a variant of libcmpc.so with extra compile flags (A/B experiments).
 #   usage: bash scripts/build_variant.sh <name> [-DFLAG ...]  -> cmpc/lib/libcmpc_<name>.so
-#   (NO_VFORM=1: without -amdgpu-mfma-vgpr-form, which crashes the compiler on the interior-point
-#    kernel variants: bash scripts/build_variant.sh ipm -DCMPC_WITH_IPM with NO_VFORM=1)
+#   (NO_VFORM=1: without -amdgpu-mfma-vgpr-form)
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift

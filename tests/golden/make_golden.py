@@ -495,7 +495,60 @@ def make_nc192_fixture(name: str = "qp_nc192.npz", want: int = 64):
     print(name, want, "instances from", seed - 2000, "batches, max KKT", KKT.max())
 
 
+def _certify_exact_one(args):
+    """The certified optimum by oracle/active_set.py, seeded with the NumPy model's answer
+    (tests/algo_spec.py; only the seed -- the certificate decides)."""
+    from oracle import active_set
+    import algo_spec
+    Ad, Bd, gd, x0, xref, contact = args
+    qp = mpc_qp.build_qp(Ad, Bd, gd, x0, xref.T, contact)
+    m = algo_spec.solve(dict(Ad=Ad, Bd=Bd, gd=gd, x0=x0, xref=xref, contact=contact),
+                        algo_spec.Params(fp32_polish=True, downdate=True, dd_max=6))
+    X = mpc_qp.rollout(Ad, Bd, gd, x0, m["U"].astype(np.float64))
+    r = active_set.certified_optimum(qp, np.concatenate([X.reshape(-1), m["U"].reshape(-1)]))
+    k = r["kkt"]
+    assert max(k.values()) < 1e-8, k
+    return r["w"], r["lam_x"], r["lam_a"], [k["stat"], k["prim"], k["comp"]]
+
+
+NEXT_TICK_NAMED = (1363, 2707, 3458, 3485)
+
+
+def _one_thread():
+    """Pool workers: one BLAS thread each (8 workers x 8 BLAS threads thrash the cores)."""
+    from threadpoolctl import threadpool_limits
+    threadpool_limits(1)
+
+
+def make_next_tick_fixture(name: str = "qp_next_tick.npz", step: int = 4):
+    """KKT-certified optima of test_warm_next_tick's batch (config 2 at 4,096, seed 2, x0 moved
+    by synth.next_tick): every `step`-th instance (1,024) plus the instances that exposed the
+    fp32 KKT check's flat-direction limit in round 4 (3458 cold: fy held at mu fz where the
+    optimum is 7.97 N, 1.48e-4; 1363 cold 6.0e-5; 2707 cold 1.34e-4 and 3485 warm 2.11e-4 with
+    the light-bin schedule on).  The interior point of oracle/tight_solver.py,
+    finished by the exact active-set solve of oracle/active_set.py.  Inputs are regenerated
+    from the deterministic generator (indices + digest); U* is stored in fp32 (the test's bar is
+    1e-4), the named instances' full (w, lam_x, lam_a) in fp64."""
+    import multiprocessing as mp
+    b = synth.next_tick(synth.make_config(2, B=4096))
+    idx = np.union1d(np.arange(0, 4096, step), np.array(NEXT_TICK_NAMED))
+    jobs = [tuple(b[k][i] for k in ("Ad", "Bd", "gd", "x0", "xref", "contact")) for i in idx]
+    with mp.get_context("fork").Pool(8, initializer=_one_thread) as pool:
+        res = pool.map(_certify_exact_one, jobs, chunksize=8)
+    W, LX, LA, KKT = (np.array(x) for x in zip(*res))
+    named = np.searchsorted(idx, NEXT_TICK_NAMED)
+    np.savez_compressed(HERE / name, idx=idx, digest=np.array(input_digest(b, idx)),
+                        U=W[:, 12 * 16:].astype(np.float32), kkt=KKT.max(1),
+                        named=np.array(NEXT_TICK_NAMED), named_w=W[named], named_lam_x=LX[named],
+                        named_lam_a=LA[named])
+    print(name, len(idx), "instances, max KKT", KKT.max())
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:  # python tests/golden/make_golden.py make_next_tick_fixture ...
+        for fn in sys.argv[1:]:
+            globals()[fn]()
+        sys.exit(0)
     make_ref_inputs()
     make_traj_ticks()
     make_leg_ticks()
@@ -505,3 +558,4 @@ if __name__ == "__main__":
     make_qp_assembly()
     make_cfg3_fixture()
     make_nc192_fixture()
+    make_next_tick_fixture()

@@ -41,7 +41,7 @@ def test_defaults_are_reference_constants(lib):
     assert abs(p.mu - 0.8) < 1e-7 and p.fz_min == 10.0                   # :15, :127
     assert abs(p.eps_abs - 1e-4) < 1e-9 and p.max_iter == 1000           # :25-27
     assert p.adaptive_rho_interval == 25                                 # :32
-    assert p.ipm_facts == 0  # interior-point fallback for hard instances: opt-in
+    assert p.reserved0 == 0  # ABI 4's ipm_facts (the interior-point fallback, removed in ABI 5)
     assert p.check_termination == 1  # OPTS check_termination (:31 has 10; include/cmpc.h says why)
     assert ctypes.sizeof(_lib.CParams) == 176  # include/cmpc.h layout (int64 max_batch at 168)
     assert _lib.CParams.max_batch.offset == 168
@@ -50,7 +50,8 @@ def test_defaults_are_reference_constants(lib):
 
 @pytest.mark.parametrize("field,value", [("N", 0), ("N", 17), ("mu", -1.0), ("max_iter", 0),
                                          ("alpha", 2.5), ("rho", 0.0), ("max_batch", 0),
-                                         ("ipm_facts", -1), ("check_termination", 0)])
+                                         ("reserved0", 8), ("reserved0", -1),
+                                         ("check_termination", 0), ("abi_version", 4)])
 def test_invalid_params_rejected_before_device(lib, field, value):
     from cmpc import _lib
     p = _lib.CParams()
@@ -62,19 +63,17 @@ def test_invalid_params_rejected_before_device(lib, field, value):
     assert "cmpc_plan_create" in lib.cmpc_last_error().decode()
 
 
-def test_default_build_has_no_interior_point_variants(lib):
-    """The product library carries only the kernels that run by default: asking for the
-    interior-point fallback (a -DCMPC_WITH_IPM variant build) is rejected before the device."""
-    import os
+def test_library_has_no_interior_point_fallback(lib):
+    """ABI 5: the interior-point fallback and its controls are gone from the library (an ABI-4
+    caller's ipm_facts > 0 is rejected as reserved0 before the device)."""
+    assert not hasattr(lib, "cmpc_plan_set_ipm") and not hasattr(lib, "cmpc_plan_ipm_batch")
     from cmpc import _lib
-    if os.environ.get("CMPC_LIB"):
-        pytest.skip("a variant library is loaded")
     p = _lib.CParams()
     lib.cmpc_params_default(ctypes.byref(p))
-    p.ipm_facts = 8
+    p.reserved0 = 8
     h = ctypes.c_void_p()
     assert lib.cmpc_plan_create(ctypes.byref(p), ctypes.byref(h)) == -22
-    assert "CMPC_WITH_IPM" in lib.cmpc_last_error().decode()
+    assert "reserved0" in lib.cmpc_last_error().decode()
 
 
 def test_null_arguments(lib):
@@ -91,7 +90,7 @@ def test_null_arguments(lib):
     assert "cmpc_leg_torque" in lib.cmpc_last_error().decode()
     assert lib.cmpc_srb_step(None, 1, 20, 0.001, *([None] * 5), 12, *([None] * 5)) == -22
     assert "cmpc_srb_step" in lib.cmpc_last_error().decode()
-    for name in ("cmpc_plan_set_team", "cmpc_plan_set_ipm", "cmpc_plan_set_heavy_first"):
+    for name in ("cmpc_plan_set_team", "cmpc_plan_set_heavy_first"):
         assert getattr(lib, name)(None, -1) == -22
         assert name in lib.cmpc_last_error().decode()
     assert lib.cmpc_plan_heavy_first_batch(None, None) == -22

@@ -85,39 +85,50 @@ def test_dual_out_is_a_kkt_multiplier(plan):
     assert dev[ok].max() < 1e-3, (dev[ok].max(), int(np.flatnonzero(ok)[dev[ok].argmax()]))
 
 
+def _rel_err_fixture(w, U_opt):
+    """max|dU| / max|U*| per instance against fp32-stored certified optima (B, 12N)."""
+    Ug = np.asarray(w, np.float64)[:, 12 * 16:]
+    Uo = np.asarray(U_opt, np.float64)
+    return np.max(np.abs(Ug - Uo), axis=1) / np.maximum(np.max(np.abs(Uo), axis=1), 1e-12)
+
+
 def test_warm_next_tick(plan):
-    """Closed-loop proxy: the next tick's problem (state moved, same reference and gait) warm-
-    started from this tick's (w, y), as centroidal_mpc.py:91-95 does without shifting.  Same
-    answer as the cold solve of the new problem, in fewer iterations on average."""
+    """Closed-loop proxy: the next tick's problem (state moved, same reference and gait;
+    synth.next_tick) cold, warm-started from this tick's (w, y) as centroidal_mpc.py:91-95 does
+    without shifting, and warm-started from this tick's REFERENCE multipliers (cmpc_solve_ref).
+    Every instance of the committed certified subset (tests/golden/qp_next_tick.npz: 1,024 of the
+    4,096 plus the four instances that exposed the fp32 check's flat-direction limit in round 4)
+    must be status 1 and within 1e-4 of its certified optimum in all three solves."""
     from cmpc import synth
+    from parity_util import input_digest
     b = synth.make_config(2, B=4096)
+    b2 = synth.next_tick(b)
+    fx = load_fixture("qp_next_tick.npz")
+    idx = fx["idx"]
+    assert input_digest(b2, idx) == str(fx["digest"])
     d = _dev(b, plan)
     w, st, it, y = _solve(plan, d, y_out=True)
-    rng = np.random.default_rng(5)
-    b2 = dict(b)
-    b2["x0"] = b["x0"] + rng.normal(scale=[2e-3] * 6 + [2e-2] * 6, size=b["x0"].shape)
+    w1, st1, it1, lam1 = _solve(plan, d, lam_out=True)
     d2 = _dev(b2, plan)
     wc, stc, itc = _solve(plan, d2)
     ww, stw, itw, yw = _solve(plan, d2, w_init=w, y_init=y, y_out=True)
+    wr, str_, itr, _ = _solve(plan, d2, w_init=w1, lam_init=lam1, lam_out=True)
+    for tag, wx, sx in (("cold", wc, stc), ("warm", ww, stw), ("warm ref", wr, str_)):
+        sn = sx.cpu().numpy()
+        assert np.all(sn[idx] == 1), (tag, np.unique(sn[idx], return_counts=True))
+        err = _rel_err_fixture(wx.cpu().numpy()[idx], fx["U"])
+        assert err.max() <= TOL_U, (tag, err.max(), int(idx[err.argmax()]))
+        for i in fx["named"]:  # the round-4 near-misses by name
+            assert err[np.searchsorted(idx, i)] <= TOL_U, (tag, int(i))
     stc, stw = stc.cpu().numpy(), stw.cpu().numpy()
     itc, itw = itc.cpu().numpy(), itw.cpu().numpy()
     assert np.mean(stw == 1) >= np.mean(stc == 1) - 1e-3
-    both = (stc == 1) & (stw == 1)
-    assert both.mean() > 0.99
-    err = rel_err_U(ww.cpu().numpy()[both], wc.cpu().numpy()[both])
-    assert err.max() <= 2 * TOL_U, (err.max(), int(np.flatnonzero(both)[err.argmax()]))
+    assert np.mean(stc == 1) > 0.99 and np.mean(stw == 1) > 0.99
     assert itw.mean() < itc.mean(), (itw.mean(), itc.mean())
     assert np.mean(itw == 0) > 0.95, np.unique(itw, return_counts=True)
     Xg, Ug = split_w(ww.cpu().numpy().astype(np.float64))
     assert feasibility(b2, Ug).max() < 1e-2
     assert np.max(np.abs(Xg - rollout64(b2, Ug))) < 1e-3
-    # certified optimum on a few instances
-    from oracle import mpc_qp, tight_solver
-    for i in (0, 1, 2, 3, 1000, 2047):
-        qp = mpc_qp.build_qp(b2["Ad"][i], b2["Bd"][i], b2["gd"][i], b2["x0"][i],
-                             b2["xref"][i].T, b2["contact"][i])
-        r = tight_solver.solve(qp)
-        assert rel_err_U(ww[i:i + 1].cpu().numpy(), r["w"][None])[0] <= TOL_U
 
 
 def test_warm_garbage_and_aliasing(plan):

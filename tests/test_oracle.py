@@ -194,3 +194,59 @@ def test_cfg3_fixture_is_kkt_certified():
                              b["contact"][i])
         k = mpc_qp.kkt_residuals(qp, fx["w"][j], fx["lam_x"][j], fx["lam_a"][j])
         assert max(k.values()) < 1e-8, (i, k)
+
+
+def test_active_set_certifier_agrees_with_the_fixtures():
+    """oracle/active_set.py (the fast certifier used on whole GPU batches) returns the fixtures'
+    certified optimum from the fixture's own answer (no step), from a seed that holds a wrong
+    face (instance 3458 of test_warm_next_tick's batch: fy held at mu fz where the optimum is
+    7.97 N -- the active-set step drops it) and from nothing (fallback to tight_solver)."""
+    from oracle import active_set
+    fx = load_fixture("qp_cfg2.npz")
+    for i in range(0, 64, 8):
+        qp = mpc_qp.build_qp(fx["Ad"][i], fx["Bd"][i], fx["gd"][i], fx["x0"][i], fx["xref"][i].T,
+                             fx["contact"][i])
+        r = active_set.certified_optimum(qp, fx["w"][i])
+        assert r["steps"] == 0 and max(r["kkt"].values()) <= active_set.CERT_TOL
+        assert np.max(np.abs(r["w"] - fx["w"][i])) <= 1e-6 * np.max(np.abs(fx["w"][i]))
+    hb = synth.make_config(2, B=4096)
+    rng = np.random.default_rng(5)
+    x0 = hb["x0"] + rng.normal(scale=[2e-3] * 6 + [2e-2] * 6, size=hb["x0"].shape)
+    i = 3458
+    qp = mpc_qp.build_qp(hb["Ad"][i], hb["Bd"][i], hb["gd"][i], x0[i], hb["xref"][i].T,
+                         hb["contact"][i])
+    opt = tight_solver.solve(qp)
+    seed = opt["w"].copy()
+    seed[192 + 12 * 9 + 3 * 3 + 1] = 8.0          # step 9, leg RR: fy on the face mu fz
+    r = active_set.certified_optimum(qp, seed)
+    assert r["steps"] >= 1 and not r["fallback"]
+    assert np.max(np.abs(r["w"] - opt["w"])) <= 1e-9 * np.max(np.abs(opt["w"]))
+    r0 = active_set.certified_optimum(qp, np.zeros(384))
+    assert max(r0["kkt"].values()) <= active_set.CERT_TOL
+    assert np.max(np.abs(r0["w"] - opt["w"])) <= 1e-6 * np.max(np.abs(opt["w"]))
+
+
+def test_next_tick_fixture_is_kkt_certified():
+    """qp_next_tick.npz (test_warm_next_tick's certified subset): the digest matches the
+    regenerated batch, the named round-4 near-misses carry KKT-certified (w, lam_x, lam_a), and a
+    sample of the stored fp32 optima are the certified optima of their instances."""
+    from oracle import active_set
+    from parity_util import input_digest
+    fx = load_fixture("qp_next_tick.npz")
+    b = synth.next_tick(synth.make_config(2, B=4096))
+    assert input_digest(b, fx["idx"]) == str(fx["digest"])
+    assert len(fx["idx"]) >= 1024 and set(fx["named"]) <= set(fx["idx"])
+    for j, i in enumerate(fx["named"]):
+        qp = mpc_qp.build_qp(b["Ad"][i], b["Bd"][i], b["gd"][i], b["x0"][i], b["xref"][i].T,
+                             b["contact"][i])
+        k = mpc_qp.kkt_residuals(qp, fx["named_w"][j], fx["named_lam_x"][j], fx["named_lam_a"][j])
+        assert max(k.values()) < 1e-8, (i, k)
+    for j in range(0, len(fx["idx"]), 97):
+        i = int(fx["idx"][j])
+        qp = mpc_qp.build_qp(b["Ad"][i], b["Bd"][i], b["gd"][i], b["x0"][i], b["xref"][i].T,
+                             b["contact"][i])
+        U = fx["U"][j].astype(np.float64)
+        X = mpc_qp.rollout(b["Ad"][i], b["Bd"][i], b["gd"][i], b["x0"][i], U.reshape(16, 12))
+        r = active_set.certified_optimum(qp, np.concatenate([X.reshape(-1), U]))
+        assert max(r["kkt"].values()) <= active_set.CERT_TOL
+        assert np.max(np.abs(r["w"][192:] - U)) <= 1e-6 * np.max(np.abs(U)), i

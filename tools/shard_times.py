@@ -21,16 +21,12 @@ def main():
     from cmpc import Plan, SolverParams, to_device_batch, synth
     from cmpc.dist import shard_bounds
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-    # IPM_FACTS: the interior-point trigger (SolverParams.ipm_facts) for trigger sweeps
-    facts = int(os.environ.get("IPM_FACTS", SolverParams.ipm_facts))
     # CMPC_PARAMS="name=value,...": other SolverParams overrides (A/B of runtime parameters)
     over = {k: type(getattr(SolverParams, k))(float(v)) for k, v in
             (a.split("=") for a in os.environ.get("CMPC_PARAMS", "").split(",") if a)}
-    plan = Plan(SolverParams(**{"max_batch": 65536, "ipm_facts": facts, **over}))
+    plan = Plan(SolverParams(**{"max_batch": 65536, **over}))
     if os.environ.get("CMPC_HEAVY_FIRST"):  # launch-order threshold (cmpc_plan_set_heavy_first)
         plan.set_heavy_first(int(os.environ["CMPC_HEAVY_FIRST"]))
-    if os.environ.get("CMPC_IPM_BATCH"):  # kernel variants with the fallback up to this batch
-        plan.set_ipm(int(os.environ["CMPC_IPM_BATCH"]))
     d = to_device_batch(synth.make_config(3))
     B = d["Ad"].shape[0]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
