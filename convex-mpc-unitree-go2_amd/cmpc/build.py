@@ -11,7 +11,7 @@ REPO = ROOT.parent
 CSRC = ROOT / "csrc"
 LIB = PKG / "lib" / "libcmpc.so"
 SOURCES = [CSRC / "cmpc_host.hip"]
-DEPS = SOURCES + [CSRC / "cmpc_wave.hip", CSRC / "cmpc_team.hip", CSRC / "cmpc_dynamics.hip", CSRC / "cmpc_traj.hip", CSRC / "cmpc_leg.hip", CSRC / "cmpc_sim.hip", CSRC / "cmpc_device.h", REPO / "include" / "cmpc.h"]
+DEPS = SOURCES + [CSRC / "cmpc_wave.hip", CSRC / "cmpc_team.hip", CSRC / "cmpc_riccati.hip", CSRC / "cmpc_dynamics.hip", CSRC / "cmpc_traj.hip", CSRC / "cmpc_leg.hip", CSRC / "cmpc_sim.hip", CSRC / "cmpc_device.h", REPO / "include" / "cmpc.h"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
 
 
@@ -42,7 +42,16 @@ def build_library(force: bool = False, verbose: bool = False) -> Path:
            f"-I{REPO / 'include'}", f"-I{CSRC}", *map(str, SOURCES), "-o", str(LIB) + ".tmp"]
     if verbose:
         print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    try:
+        subprocess.run(cmd, check=True)
+    except subprocess.CalledProcessError:
+        # -amdgpu-mfma-vgpr-form is an internal LLVM option: a compiler that rejects it (or
+        # crashes on a kernel with it) still builds the library, at the spills it avoided
+        vf = cmd.index("-amdgpu-mfma-vgpr-form")
+        cmd = cmd[:vf - 1] + cmd[vf + 1:]
+        print("cmpc.build: WARNING: hipcc failed with -mllvm -amdgpu-mfma-vgpr-form; retrying "
+              "without it (the one-wave-per-SIMD kernels will spill)")
+        subprocess.run(cmd, check=True)
     os.replace(str(LIB) + ".tmp", LIB)
     return LIB
 

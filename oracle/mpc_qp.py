@@ -12,10 +12,13 @@ Pinning:
   * inputs (contact table, Ac/Bc, Ad/Bd/gd, x_ref) are pinned against golden vectors produced
     by running the reference's own ``gait.py`` / ``com_trajectory.py`` code
     (``tests/golden/make_golden.py``);
-  * the QP assembly (H, g, A, bounds) is pinned against the structural invariants the
-    reference prints at init (``centroidal_mpc.py:225-230``: H 384x384 nnz 384, A 448x384
-    nnz 5168 dens 0.0300) -- CasADi is not installed, so values cannot be compared with a
-    CasADi run ("assembly values parity unpinned beyond the invariants").
+  * the QP assembly (H, g, A, lba/uba, lbx/ubx and the init print) is pinned by the
+    reference's own ``CentroidalMPC`` (``centroidal_mpc.py:41-67, 122-359``) run unmodified
+    under a conversion-only casadi stand-in (``tests/golden/casadi_standin.py``): the golden
+    vectors in ``tests/golden/qp_assembly.npz`` (``make_golden.make_qp_assembly``) equal this
+    module's ``build_qp`` to 1e-14 on 100 instances (``tests/test_oracle.py``), besides the
+    structural invariants the reference prints (H 384x384 nnz 384, A 448x384 nnz 5168 dens
+    0.0300).  Only OSQP's own iterate stays unpinnable (CasADi/OSQP are not installed).
 """
 from __future__ import annotations
 

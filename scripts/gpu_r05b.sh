@@ -5,6 +5,8 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 L=convex-mpc-unitree-go2_amd/cmpc/lib
+timeout -k 10 600 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?; tail -1 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || { grep -E "^FAILED|Error|assert" gpurun_out/gpu_tests.log | head -20; exit 1; }
 for i in ${TRACE_IDS:-54289 21027 52595}; do
   timeout -k 10 120 python -u tools/trace_instance.py $i 3 > gpurun_out/trace_cfg3_$i.txt 2>&1 || { tail -5 gpurun_out/trace_cfg3_$i.txt; exit 1; }
 done
@@ -12,8 +14,8 @@ SETS=${SETS:-cfg3_65536,cfg3_next_warm,cfg2_next_cold}
 CMPC_LIB=$L/libcmpc_r04.so CMPC_ALLOW_ABI4=1 SURVEY_DIR=/tmp/sv_r04 timeout -k 10 300 python -u tests/certify_sample.py gpu --sets $SETS > gpurun_out/survey_r04_gpu.log 2>&1 || { tail -5 gpurun_out/survey_r04_gpu.log; exit 1; }
 SURVEY_DIR=/tmp/sv_r04 timeout -k 10 900 python -u tests/certify_sample.py cpu --sets $SETS --report gpurun_out/r04lib/parity_survey.txt > gpurun_out/survey_r04_cpu.log 2>&1 || { tail -5 gpurun_out/survey_r04_cpu.log; exit 1; }
 grep -E "above 1e-4|^cfg" gpurun_out/survey_r04_cpu.log
-timeout -k 10 300 python -u tests/certify_sample.py gpu --sets $SETS > gpurun_out/survey_gpu.log 2>&1 || { tail -5 gpurun_out/survey_gpu.log; exit 1; }
-timeout -k 10 900 python -u tests/certify_sample.py cpu --sets $SETS > gpurun_out/survey_cpu.log 2>&1 || { tail -5 gpurun_out/survey_cpu.log; exit 1; }
+timeout -k 10 300 python -u tests/certify_sample.py gpu > gpurun_out/survey_gpu.log 2>&1 || { tail -5 gpurun_out/survey_gpu.log; exit 1; }
+timeout -k 10 900 python -u tests/certify_sample.py cpu > gpurun_out/survey_cpu.log 2>&1 || { tail -5 gpurun_out/survey_cpu.log; exit 1; }
 grep -E "above 1e-4|^cfg|status" gpurun_out/survey_cpu.log
 W="--cpu-seconds 0 --sub-configs 0 --dynamics-steps 0 --tick-steps 0 --leg-steps 0 --loop-steps 0 --api-ticks 0 --steps 5"
 for v in "$L/libcmpc_r04.so" "$L/libcmpc.so" "$L/libcmpc.so@CMPC_TOP_GRID=64"; do

@@ -110,6 +110,7 @@ def _one(i):
 def cpu(sets, procs, report):
     global _B, _U
     lines, worst_all = [], {}
+    Path(report).parent.mkdir(parents=True, exist_ok=True)
     for name in sets:
         t0 = time.time()
         first = len(lines)

@@ -213,3 +213,34 @@ def test_general_step_matrix(plan, reps):
     for i in range(8):
         wr = _tight(b, i)
         assert rel_err_U(w[i * reps:i * reps + 1], wr[None])[0] <= TOL_U, i
+
+
+def test_general_step_matrix_heavy_bins(plan):
+    """The general-A path (the squared-power gradient scans and forward condensation, fp32
+    rollout) on the NC 144 / 160 / 192 kernels and the hard instances (face-downdate repairs):
+    the attitude-damped Ad of test_general_step_matrix on the cfg2 fixtures' heavier instances,
+    16 of the NC 192 fixtures and the four hard cases, replicated past the small-batch bound so
+    that the one-wave group kernels run them.  Every instance is certified on the CPU against
+    its own KKT-certified optimum (oracle/active_set.py, seeded by the GPU's answer).  A general
+    A keeps the relative multiplier test: a loose acceptance there is status 2."""
+    from cmpc import solve_batch
+    from oracle import active_set, mpc_qp
+    keys = ("Ad", "Bd", "gd", "x0", "xref", "contact")
+    c2, c192, hd = load_fixture("qp_cfg2.npz"), load_fixture("qp_nc192.npz"), load_fixture("qp_hard.npz")
+    heavy = np.flatnonzero(3 * (c2["contact"] != 0).reshape(len(c2["contact"]), -1).sum(1) > 128)[:12]
+    b = {k: np.concatenate([c2[k][heavy], c192[k][:16], hd[k]]).astype(np.float64) for k in keys}
+    for r in range(3, 6):
+        b["Ad"][:, r, r] = 0.999
+    B0, reps = len(b["Ad"]), 96
+    big = {k: np.repeat(v, reps, axis=0) for k, v in b.items()}
+    w, st, it = solve_batch(big, plan=plan)
+    assert np.mean(st == 1) > 0.99 and np.all((st == 1) | (st == 2)), np.unique(st, return_counts=True)
+    for i in range(B0):
+        qp = mpc_qp.build_qp(b["Ad"][i], b["Bd"][i], b["gd"][i], b["x0"][i], b["xref"][i].T,
+                             b["contact"][i])
+        wi = w[i * reps].astype(np.float64)
+        r = active_set.certified_optimum(qp, wi)
+        assert max(r["kkt"].values()) <= active_set.CERT_TOL, i
+        errs = rel_err_U(w[i * reps:(i + 1) * reps], np.repeat(r["w"][None], reps, axis=0))
+        ok = st[i * reps:(i + 1) * reps] == 1
+        assert errs[ok].max() <= TOL_U, (i, errs.max())

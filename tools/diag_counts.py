@@ -34,13 +34,15 @@ def main():
         torch.cuda.synchronize()
         cyc = st.cpu().numpy().astype(np.float64) * 16
         code = it.cpu().numpy().astype(np.int64)
-        iters, pol, fac = code % 1000, (code // 1000) % 1000, code // 1000000
+        iters, polraw, fac = code % 1000, (code // 1000) % 1000, code // 1000000
+        loose, pol = polraw // 100, polraw % 100   # (+100 per loose acceptance, cmpc_wave.hip)
         if os.environ.get("CMPC_DIAG_SAVE"):
             np.savez_compressed(f"{os.environ['CMPC_DIAG_SAVE']}_cfg{cfg}.npz", cyc=cyc, code=code)
         order = np.argsort(-cyc)
         tot = cyc.sum()
         print(f"cfg{cfg} {over}: mean cycles {cyc.mean():.0f}  iters mean {iters.mean():.2f}  "
-              f"polish {pol.mean():.2f}  fact {fac.mean():.2f}")
+              f"polish {pol.mean():.2f}  fact {fac.mean():.2f}  loose acceptances "
+              f"{int((loose > 0).sum())} of {len(cyc)}")
         for frac in (0.001, 0.01, 0.05):
             k = max(1, int(frac * len(cyc)))
             top = order[:k]
