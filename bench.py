@@ -137,6 +137,9 @@ def parse(argv=None):
                     help="small-batch team mode for B <= this (cmpc_plan_set_team): -1 auto, 0 off")
     ap.add_argument("--heavy-first", type=int, default=int(os.environ.get("CMPC_HEAVY_FIRST", "-1")),
                     help="NC >= 160 class first for B >= this (cmpc_plan_set_heavy_first): -1 auto, 0 never")
+    ap.add_argument("--stance-all", action="store_true",
+                    help="experiments: every foot in stance at every step (a standing batch: "
+                         "every instance in the NC 192 bin)")
     ap.add_argument("--lib", type=str, default=None,
                     help="alternative build of libcmpc.so (A/B experiments)")
     a = ap.parse_args(argv)
@@ -365,6 +368,8 @@ def main(argv=None):
     else:
         full = synth.make_batch(GB, seed=synth.CONFIGS[cfg]["seed"] + args.seed_offset,
                                 mixed=synth.CONFIGS[cfg]["mixed"])
+    if args.stance_all:
+        full["contact"] = np.ones_like(full["contact"])
     lo, hi = cdist.shard_bounds(GB, rank, world)
     shard = {k: full[k][lo:hi] for k in cdist.FIELDS}
     Bs = hi - lo
@@ -520,6 +525,7 @@ def main(argv=None):
                                     + ("trot 3Hz/0.6 + mixed stance masks interleaved"
                                        if cfg == 3 else "trot 3Hz/0.6 fixed schedule" if cfg == 1
                                        else "mixed stance masks")
+                                    + (" (EXPERIMENT: all feet in stance)" if args.stance_all else "")
                                     + f", one global batch sharded over {world} rank(s), "
                                       "inputs resident in HBM"),
                        "N": 16, "global_batch": GB, "batch_per_gpu": Bs,

@@ -309,11 +309,15 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
                     cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
 }
 
+// group k's persistent kernel with g waves whose park slabs start at wave w0 of the group's
+// region (a second launch of the same group on the same queue heads takes the slabs after the
+// first one's); `timed` records the launch for cmpc_plan_timing_read
 static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParams& kp,
-                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g) {
+                         const cmpc::Inputs& in, const cmpc::Outputs& out, unsigned g,
+                         unsigned w0 = 0, bool timed = true) {
   hipError_t e;
   cmpc_plan::Rec rec{nullptr, nullptr, k};
-  const bool rec_this = pl->timing && pl->recs.size() < 4096 * kNumGroups;
+  const bool rec_this = timed && pl->timing && pl->recs.size() < 4096 * kNumGroups;
   if (rec_this) {
     if (!pl->pool.empty()) {
       rec = pl->pool.back();
@@ -329,8 +333,8 @@ static int record_launch(cmpc_plan* pl, int k, hipStream_t s, const cmpc::KParam
   hipLaunchKernelGGL(group_fn(k), dim3(g), dim3(64), 0, s, kp, in, out,
                      pl->d_lists + (size_t)qa * pl->p.max_batch,
                      pl->d_lists + (size_t)(qa - 1) * pl->p.max_batch, pl->d_counters,
-                     pl->d_counters + cmpc::kNumBins, qa, pl->d_work + pl->work_off[k],
-                     pl->slab[k]);
+                     pl->d_counters + cmpc::kNumBins, qa,
+                     pl->d_work + pl->work_off[k] + (size_t)w0 * pl->slab[k], pl->slab[k]);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "solve_group_kernel launch");
   if (rec_this) {
@@ -441,11 +445,15 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   // (config 2 at 4,096: 2.0 vs 2.4 ms) keep the NC <= 128 class first.  Heavy-first relies on
   // the LDS slot padding of solve_group_kernel (cmpc_wave.hip kLdsSlot): without it the
   // NC <= 128 waves that replace the NC >= 160 ones fit ~6 instead of 8 per CU.
-  // The NC 192 bin (rare: one instance in config 3's 65,536) has its own kernel on the second
-  // plan stream, submitted before the classes so that its waves -- which exit at once when the
-  // bin is empty -- are dispatched before the classes fill the SIMDs, and its instances start
-  // at the beginning of the step (a one-wave-per-SIMD wave could not start later, with the
-  // SIMDs held by two-wave NC <= 128 waves).
+  // The NC 192 bin (rare: one instance in config 3's 65,536, but every instance of a standing
+  // batch) has its own kernel in two launches on the same queue: a few waves (one per 4 CUs)
+  // on the second plan stream, submitted before the classes so that they are dispatched before
+  // the classes fill the SIMDs and the bin's instances start at the beginning of the step (a
+  // one-wave-per-SIMD wave could not start later, with the SIMDs held by two-wave NC <= 128
+  // waves); then the rest of the grid on the caller's stream once both classes are done, to
+  // drain what the few waves have not taken.  An empty bin costs one dispatch of waves that
+  // exit at once on an idle device, instead of 1,024 whole-SIMD waves that trickle in as the
+  // classes free their SIMDs (a 5 ms span with 0 instances, round 4).
   const bool big = has_group(pl, 1), top = has_group(pl, 2);
   if (big) {
     if ((e = hipEventRecord(pl->fork, st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -456,12 +464,9 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
   }
   unsigned gk[kNumGroups];
   for (int k = 0; k < kNumGroups; ++k) gk[k] = (unsigned)(pl->grid[k] < B ? pl->grid[k] : B);
-  {  // (experiment knob CMPC_TOP_GRID: cap the NC 192 kernel's persistent grid)
-    static const int cap = [] { const char* v = getenv("CMPC_TOP_GRID"); return v ? atoi(v) : 0; }();
-    if (cap > 0 && gk[2] > (unsigned)cap) gk[2] = (unsigned)cap;
-  }
+  const unsigned top_early = std::min(gk[2], (unsigned)std::max(1, pl->cus / 4));
   if (top) {
-    rc = record_launch(pl, 2, pl->top, kp, in, out, gk[2]);
+    rc = record_launch(pl, 2, pl->top, kp, in, out, top_early);
     if (rc != CMPC_OK) return rc;
   }
   const int64_t hmin = heavy_first_batch(pl);
@@ -474,6 +479,10 @@ static int solve_impl(cmpc_plan* pl, int64_t B, const cmpc::Inputs& in, const cm
     if ((e = hipEventRecord(pl->join, pl->side)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     if ((e = hipStreamWaitEvent(st, pl->join, 0)) != hipSuccess)
       return hip_fail(e, "hipStreamWaitEvent");
+    if (top && gk[2] > top_early) {
+      rc = record_launch(pl, 2, st, kp, in, out, gk[2] - top_early, top_early, false);
+      if (rc != CMPC_OK) return rc;
+    }
     if (top) {
       if ((e = hipEventRecord(pl->join_top, pl->top)) != hipSuccess) return hip_fail(e, "hipEventRecord");
       if ((e = hipStreamWaitEvent(st, pl->join_top, 0)) != hipSuccess)

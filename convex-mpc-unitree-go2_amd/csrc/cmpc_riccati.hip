@@ -99,8 +99,9 @@ template <int NC, int k>
 __device__ __forceinline__ void ric_factor_step(Smem<NC>& s, RicRegs& F, f4& W, int N, float shift,
                                                 const float (&adB)[3], const float (&adA)[3],
                                                 const float (&q2d)[3], int g, int rc) {
-  if (k < N) {  // uniform
-    const int p0 = s.off[k], m = s.off[k + 1] - p0;
+  {
+    const bool act = k < N;  // uniform (a step past the horizon: m = 0, W kept)
+    const int p0 = act ? s.off[k] : 0, m = act ? s.off[k + 1] - p0 : 0;
     const bool cv = rc >= 0 && rc < m;
     float bq[3], ba[3];  // B~[3g+q][rc] (D layout of B~), B~[rc][3g+q] (of B~')
 #pragma unroll
@@ -158,7 +159,7 @@ __device__ __forceinline__ void ric_factor_step(Smem<NC>& s, RicRegs& F, f4& W, 
     }
     if constexpr (k > 0) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) W[q] = V0[q] - GK[q] + q2d[q];
+      for (int q = 0; q < 3; ++q) W[q] = act ? V0[q] - GK[q] + q2d[q] : W[q];
     }
   }
   if constexpr (k > 0) ric_factor_step<NC, k - 1>(s, F, W, N, shift, adB, adA, q2d, g, rc);
@@ -185,114 +186,117 @@ __device__ __forceinline__ void ric_factor(Smem<NC>& s, const KParams& P, RicReg
   ric_factor_step<NC, kMaxN - 1>(s, F, W, uniform(P.N), shift, adB, adA, q2d, g, rc);
 }
 
-// backward sweep step k: p_k = Phi_k' p_{k+1} + K_k' r_k; q_k = S_k^-1 (B~_k' p_{k+1} - r_k) -> out
+// backward sweep step k: p_k = Phi_k' p_{k+1} + K_k' r_k; q_k = S_k^-1 (B~_k' p_{k+1} - r_k)
+// -> qv.  The step's loads do not depend on the chain and no step is a branch of its own (a
+// step past the horizon has m = 0 and keeps p), so the compiler can issue them early.
 template <int NC, int k>
-__device__ __forceinline__ void ric_bwd(Smem<NC>& s, int N, const RicRegs& F, const float* in,
-                                        float* out, float& pC, float (&pR)[3], int g, int c,
-                                        int rc) {
-  if (k < N) {  // uniform
-    const int p0 = s.off[k], m = s.off[k + 1] - p0;
-    const bool cv = rc >= 0 && rc < m;
-    float rR[3];
+__device__ __forceinline__ void ric_bwd(Smem<NC>& s, int N, const RicRegs& F,
+                                        const float* __restrict__ in, float* __restrict__ qv,
+                                        float& pC, float (&pR)[3], int g, int c, int rc) {
+  const bool act = k < N;  // uniform
+  const int p0 = act ? s.off[k] : 0, m = act ? s.off[k + 1] - p0 : 0;
+  const bool cv = rc >= 0 && rc < m;
+  float rR[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) rR[q] = (3 * g + q < m) ? in[p0 + 3 * g + q] : 0.f;
-    const float rC = cv ? in[p0 + rc] : 0.f;
-    if constexpr ((k & 1) == 0) {  // p_{k+1} R -> p_k C
-      float bq[3];
+  for (int q = 0; q < 3; ++q) rR[q] = (3 * g + q < m) ? in[p0 + 3 * g + q] : 0.f;
+  const float rC = cv ? in[p0 + rc] : 0.f;
+  if constexpr ((k & 1) == 0) {  // p_{k+1} R -> p_k C
+    float bq[3];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) bq[q] = cv ? s.Bt[(p0 + rc) * kBS + 3 * g + q] : 0.f;
-      float t = 0.f, tb = 0.f;
+    for (int q = 0; q < 3; ++q) bq[q] = cv ? s.Bt[(p0 + rc) * kBS + 3 * g + q] : 0.f;
+    float t = 0.f, tb = 0.f;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        t = fmaf(F.y[k][q], pR[q], fmaf(F.z[k][q], rR[q], t));
-        tb = fmaf(bq[q], pR[q], tb);
-      }
-      const float bC = col4_sum(tb) - rC;
-      pC = col4_sum(t);
-      float qR[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) qR[q] = row16_sum(F.si[k][q] * bC);
-      if (c == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (3 * g + q < m) out[p0 + 3 * g + q] = qR[q];
-      }
-    } else {  // p_{k+1} C -> p_k R
-      float ba[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        ba[q] = (rc >= 0 && 3 * g + q < m) ? s.Bt[(p0 + 3 * g + q) * kBS + rc] : 0.f;
-      float bR[3], pn[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        pn[q] = row16_sum(fmaf(F.y[k][q], pC, F.z[k][q] * rC));
-        bR[q] = row16_sum(ba[q] * pC) - rR[q];
-      }
-      float tq = 0.f;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) tq = fmaf(F.si[k][q], bR[q], tq);
-      const float qC = col4_sum(tq);
-      if (g == 0 && cv) out[p0 + rc] = qC;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) pR[q] = pn[q];
+    for (int q = 0; q < 3; ++q) {
+      t = fmaf(F.y[k][q], pR[q], fmaf(F.z[k][q], rR[q], t));
+      tb = fmaf(bq[q], pR[q], tb);
     }
-  }
-  if constexpr (k > 0) ric_bwd<NC, k - 1>(s, N, F, in, out, pC, pR, g, c, rc);
-}
-
-// forward sweep step k: e_{k+1} = Phi_k e_k - B~_k q_k,  v_k = -K_k e_k - q_k (over q_k in out)
-template <int NC, int k>
-__device__ __forceinline__ void ric_fwd(Smem<NC>& s, int N, const RicRegs& F, float* out,
-                                        float& eC, float (&eR)[3], int g, int c, int rc) {
-  if (k < N) {  // uniform
-    const int p0 = s.off[k], m = s.off[k + 1] - p0;
-    const bool cv = rc >= 0 && rc < m;
+    const float bC = col4_sum(tb) - rC;
+    const float pn = col4_sum(t);
+    pC = act ? pn : pC;
     float qR[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) qR[q] = (3 * g + q < m) ? out[p0 + 3 * g + q] : 0.f;
-    const float qC = cv ? out[p0 + rc] : 0.f;
-    WSYNC();  // (q_k read by every lane before v_k overwrites it)
-    if constexpr ((k & 1) == 0) {  // e_k C -> e_{k+1} R
-      float bq[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) bq[q] = cv ? s.Bt[(p0 + rc) * kBS + 3 * g + q] : 0.f;
-      float en[3], vR[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        en[q] = row16_sum(fmaf(F.y[k][q], eC, -bq[q] * qC));
-        vR[q] = -row16_sum(F.z[k][q] * eC) - qR[q];
-      }
-      if (c == 0) {
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (3 * g + q < m) out[p0 + 3 * g + q] = vR[q];
-      }
-#pragma unroll
-      for (int q = 0; q < 3; ++q) eR[q] = en[q];
-    } else {  // e_k R -> e_{k+1} C
-      float ba[3];
+    for (int q = 0; q < 3; ++q) qR[q] = row16_sum(F.si[k][q] * bC);
+    if (c == 0) {
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        ba[q] = (rc >= 0 && 3 * g + q < m) ? s.Bt[(p0 + 3 * g + q) * kBS + rc] : 0.f;
-      float te = 0.f, tk = 0.f;
-#pragma unroll
-      for (int q = 0; q < 3; ++q) {
-        te = fmaf(F.y[k][q], eR[q], fmaf(-ba[q], qR[q], te));
-        tk = fmaf(F.z[k][q], eR[q], tk);
-      }
-      const float vC = -col4_sum(tk) - qC;
-      eC = col4_sum(te);
-      if (g == 0 && cv) out[p0 + rc] = vC;
+        if (3 * g + q < m) qv[p0 + 3 * g + q] = qR[q];
     }
+  } else {  // p_{k+1} C -> p_k R
+    float ba[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      ba[q] = (rc >= 0 && 3 * g + q < m) ? s.Bt[(p0 + 3 * g + q) * kBS + rc] : 0.f;
+    float bR[3], pn[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      pn[q] = row16_sum(fmaf(F.y[k][q], pC, F.z[k][q] * rC));
+      bR[q] = row16_sum(ba[q] * pC) - rR[q];
+    }
+    float tq = 0.f;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) tq = fmaf(F.si[k][q], bR[q], tq);
+    const float qC = col4_sum(tq);
+    if (g == 0 && cv) qv[p0 + rc] = qC;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pR[q] = act ? pn[q] : pR[q];
   }
-  if constexpr (k + 1 < kMaxN) ric_fwd<NC, k + 1>(s, N, F, out, eC, eR, g, c, rc);
+  if constexpr (k > 0) ric_bwd<NC, k - 1>(s, N, F, in, qv, pC, pR, g, c, rc);
 }
 
-// out = (H + shift I)^-1 in over the first n params (out is zero beyond n); in must not alias
-// out.  Registers and the two param vectors only.
+// forward sweep step k: e_{k+1} = Phi_k e_k - B~_k q_k,  v_k = -K_k e_k - q_k -> vv
+template <int NC, int k>
+__device__ __forceinline__ void ric_fwd(Smem<NC>& s, int N, const RicRegs& F,
+                                        const float* __restrict__ qv, float* __restrict__ vv,
+                                        float& eC, float (&eR)[3], int g, int c, int rc) {
+  const bool act = k < N;  // uniform
+  const int p0 = act ? s.off[k] : 0, m = act ? s.off[k + 1] - p0 : 0;
+  const bool cv = rc >= 0 && rc < m;
+  float qR[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) qR[q] = (3 * g + q < m) ? qv[p0 + 3 * g + q] : 0.f;
+  const float qC = cv ? qv[p0 + rc] : 0.f;
+  if constexpr ((k & 1) == 0) {  // e_k C -> e_{k+1} R
+    float bq[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) bq[q] = cv ? s.Bt[(p0 + rc) * kBS + 3 * g + q] : 0.f;
+    float en[3], vR[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      en[q] = row16_sum(fmaf(F.y[k][q], eC, -bq[q] * qC));
+      vR[q] = -row16_sum(F.z[k][q] * eC) - qR[q];
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (3 * g + q < m) vv[p0 + 3 * g + q] = vR[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) eR[q] = act ? en[q] : eR[q];
+  } else {  // e_k R -> e_{k+1} C
+    float ba[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      ba[q] = (rc >= 0 && 3 * g + q < m) ? s.Bt[(p0 + 3 * g + q) * kBS + rc] : 0.f;
+    float te = 0.f, tk = 0.f;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      te = fmaf(F.y[k][q], eR[q], fmaf(-ba[q], qR[q], te));
+      tk = fmaf(F.z[k][q], eR[q], tk);
+    }
+    const float vC = -col4_sum(tk) - qC;
+    const float en = col4_sum(te);
+    eC = act ? en : eC;
+    if (g == 0 && cv) vv[p0 + rc] = vC;
+  }
+  if constexpr (k + 1 < kMaxN) ric_fwd<NC, k + 1>(s, N, F, qv, vv, eC, eR, g, c, rc);
+}
+
+// out = (H + shift I)^-1 in over the first n params (out is zero beyond n).  in must not alias
+// out and is CLOBBERED (the forward sweep writes v there, then v is copied to out: the two
+// sweeps read one buffer and write the other, so their loads issue early).
 template <int NC>
 __device__ __forceinline__ void ric_apply(Smem<NC>& s, int N, const RicRegs& F, int n,
-                                          const float* in, float* out) {
+                                          float* __restrict__ in, float* __restrict__ out) {
   CMPC_T0(t_sv);
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
@@ -301,11 +305,12 @@ __device__ __forceinline__ void ric_apply(Smem<NC>& s, int N, const RicRegs& F, 
   N = uniform(N);
   WSYNC();
   float pC = 0.f, pR[3] = {0.f, 0.f, 0.f};  // p_N = 0
-  ric_bwd<NC, kMaxN - 1>(s, N, F, in, out, pC, pR, g, c, rc);
+  ric_bwd<NC, kMaxN - 1>(s, N, F, in, out, pC, pR, g, c, rc);   // q -> out
   WSYNC();
   float eC = 0.f, eR[3] = {0.f, 0.f, 0.f};  // e_0 = 0
-  ric_fwd<NC, 0>(s, N, F, out, eC, eR, g, c, rc);
-  for (int p = n + lane; p < NC; p += 64) out[p] = 0.f;
+  ric_fwd<NC, 0>(s, N, F, out, in, eC, eR, g, c, rc);           // v -> in
+  WSYNC();
+  for (int p = lane; p < NC; p += 64) out[p] = (p < n) ? in[p] : 0.f;
   WSYNC();
   CMPC_ACC(3, t_sv);
   CMPC_CNT(13, 1);

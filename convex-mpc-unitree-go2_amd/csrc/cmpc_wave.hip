@@ -44,6 +44,14 @@ namespace cmpc {
 #ifndef CMPC_RICCATI
 #define CMPC_RICCATI 0
 #endif
+// ... or only the bins with NC >= CMPC_RICCATI_MIN_NC (0: none)
+#ifndef CMPC_RICCATI_MIN_NC
+#define CMPC_RICCATI_MIN_NC 0
+#endif
+template <int NC>
+constexpr bool ric_for() {
+  return CMPC_RICCATI || (CMPC_RICCATI_MIN_NC > 0 && NC >= CMPC_RICCATI_MIN_NC);
+}
 
 #ifndef CMPC_WPE_OVERRIDE
 #define CMPC_WPE_OVERRIDE ((4 * NTL <= 150) ? 2 : 1)
@@ -204,7 +212,7 @@ struct Cfg {
   static constexpr int NTL = TT * (TT + 1) / 2;  // lower-triangle tiles (f4 per lane each)
   static constexpr int THREADS = 64;             // one wave per QP
   // per wave (floats): park slab of the inverse (or of the Riccati factors: 144 per lane)
-  static constexpr int SLAB = (CMPC_RICCATI && NTL * 256 < 144 * 64) ? 144 * 64 : NTL * 256;
+  static constexpr int SLAB = (ric_for<NC>() && NTL * 256 < 144 * 64) ? 144 * 64 : NTL * 256;
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
   static constexpr int WPE = CMPC_WPE_OVERRIDE;
 };
@@ -289,7 +297,6 @@ constexpr float kLooseTol = 5.f;
 #define CMPC_WARM_RESTART 1
 #endif
 constexpr bool kWarmRestart = CMPC_WARM_RESTART;
-constexpr bool kRiccati = CMPC_RICCATI;
 // Face multipliers in force units (polish_check, nilpotent step with the float64 rollout): a
 // held face's multiplier must be >= -kFaceErr x polish_tol x us x R2 (a force error of at most
 // ~5e-5 relative once released); a loose acceptance allows kLooseFace x that and is status 1
@@ -1448,9 +1455,10 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
   CMPC_CNT(12, 1);
 }
 
-#include "cmpc_riccati.hip"  // (H + shift I)^-1 as a Riccati factorization (kRiccati)
+#include "cmpc_riccati.hip"  // (H + shift I)^-1 as a Riccati factorization (ric_for)
 
-// M applied to a param vector: the register-tile inverse, or the Riccati sweeps
+// M applied to a param vector: the register-tile inverse, or the Riccati sweeps (which clobber
+// `in`)
 template <int NC, int NT>
 __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const f4 (&M)[NT], int n,
                                            const float* in, float* out) {
@@ -1459,7 +1467,9 @@ __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const 
 template <int NC>
 __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const RicRegs& F, int n,
                                            const float* in, float* out) {
-  ric_apply<NC>(s, P.N, F, n, in, out);
+  // (every caller's `in` is dead after the apply: the ADMM right-hand side s.r, the
+  // refinement's gradient s.g, a downdate's face vector s.r)
+  ric_apply<NC>(s, P.N, F, n, const_cast<float*>(in), out);
 }
 
 // Euclidean projection of (a, b, c) onto {|x| <= mu z, |y| <= mu z, z >= fz_min}.
@@ -1985,7 +1995,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
                                                int* seq) {
   // W = 1: the whole lower triangle in this wave's registers (or the Riccati factors);
   // W > 1: this wave's team slots
-  using MinvT = typename std::conditional<(W == 1 && kRiccati), RicRegs,
+  using MinvT = typename std::conditional<(W == 1 && ric_for<NC>()), RicRegs,
                                           f4[TeamCfg<NC, W>::SLOTS]>::type;
   MinvT M;
   static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
@@ -2167,7 +2177,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #ifdef CMPC_DIAG_COUNTS
       ++dg_fact;
 #endif
-      if constexpr (W == 1 && kRiccati) {
+      if constexpr (W == 1 && ric_for<NC>()) {
         CMPC_T0(t_c);
         ric_factor<NC>(s, P, M, nact, uniformf(shift));
         CMPC_ACC(0, t_c);
