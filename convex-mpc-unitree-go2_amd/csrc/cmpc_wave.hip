@@ -52,6 +52,16 @@ template <int NC>
 constexpr bool ric_for() {
   return CMPC_RICCATI || (CMPC_RICCATI_MIN_NC > 0 && NC >= CMPC_RICCATI_MIN_NC);
 }
+// The one-wave kernels of the bins with NC >= CMPC_LDL_MIN_NC keep a block LDL' factorization
+// of (H + shift I) in the register tiles instead of its inverse (invert_tiles<NC, true>,
+// ldl_apply); 0: none
+#ifndef CMPC_LDL_MIN_NC
+#define CMPC_LDL_MIN_NC 0
+#endif
+template <int NC>
+constexpr bool ldl_for() {
+  return !ric_for<NC>() && CMPC_LDL_MIN_NC > 0 && NC >= CMPC_LDL_MIN_NC;
+}
 
 #ifndef CMPC_WPE_OVERRIDE
 #define CMPC_WPE_OVERRIDE ((4 * NTL <= 150) ? 2 : 1)
@@ -488,7 +498,7 @@ constexpr int kSweepPipeMaxNC = CMPC_SWEEP_PIPE_MAX_NC;
 // Each step issues its MFMAs on those tiles first, publishes the next panel from them, and then
 // issues the remaining MFMAs of the step in the same basic block as the next step's LDL and
 // operand build, so that serial chain fills the gaps between MFMAs instead of stalling the wave.
-template <int NC, int K, class SM>
+template <int NC, int K, bool LDL, class SM>
 __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL], int sub,
                                               int g, int c) {
   using C = Cfg<NC>;
@@ -507,7 +517,7 @@ __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL]
       for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
     }
   }
-  if (roww) {
+  if (!LDL && roww) {  // (the factorization never reads the swept rows above the block)
 #pragma unroll
     for (int J = 0; J < K; ++J) *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(K, J)];
   }
@@ -515,7 +525,7 @@ __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL]
 }
 
 // LDL of the 4x4 pivot block (rows k0..k0+3 of the panel) and the step's MFMA operands
-template <int NC, class SM>
+template <int NC, int KMIN, class SM>
 __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
                                                float (&a)[Cfg<NC>::TT], float (&b)[Cfg<NC>::TT]) {
   using C = Cfg<NC>;
@@ -528,7 +538,7 @@ __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
   }
   f4 ph[C::TT];
 #pragma unroll
-  for (int I = 0; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
+  for (int I = KMIN; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
   // (inline: factored into a helper returning a struct, the compiler spilled an operand in
   // every sweep step, 28 scratch stores and loads in the NC <= 128 kernel)
   const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
@@ -550,7 +560,7 @@ __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
   const float w3 = g3 ? 1.f : 0.f;
   const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
 #pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
+  for (int I = KMIN; I < C::TT; ++I) {
     const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
     a[I] = -yg;
     b[I] = yg * ig;
@@ -558,16 +568,16 @@ __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
 }
 
 // rank-4 update of the tiles whose criticality for pivot block Kc is CRIT
-template <int NC, int Kc, bool CRIT>
+template <int NC, int Kc, bool CRIT, bool LDL, int KMIN>
 __device__ __forceinline__ void sweep_mfma(f4 (&M)[Cfg<NC>::NTL], const float (&a)[Cfg<NC>::TT],
                                            const float (&b)[Cfg<NC>::TT], int TA) {
   using C = Cfg<NC>;
 #pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
+  for (int I = KMIN; I < C::TT; ++I) {
     if (I >= TA) continue;  // uniform
 #pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      const bool crit = (J == Kc && I >= Kc) || (I == Kc && J < Kc);
+    for (int J = KMIN; J <= I; ++J) {
+      const bool crit = (J == Kc && I >= Kc) || (!LDL && I == Kc && J < Kc);
       if (crit != CRIT) continue;  // compile-time after unrolling
       const int t = tile_index(I, J);
       M[t] = mfma4(a[I], b[J], M[t]);
@@ -584,34 +594,37 @@ __device__ __forceinline__ void sweep_diagfix(f4 (&M)[Cfg<NC>::NTL], int sub, in
   for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
 }
 
-template <int NC, int K, class SM>
+template <int NC, int K, bool LDL, class SM>
 __device__ __forceinline__ void sweep_block(SM& s, f4 (&M)[Cfg<NC>::NTL], int ng, int TA,
                                             int g, int c, float (&a)[Cfg<NC>::TT],
                                             float (&b)[Cfg<NC>::TT]) {
   using C = Cfg<NC>;
+  constexpr int KM = LDL ? K : 0;  // first tile column the block's steps update
   if constexpr (K < C::TT) {
     if (4 * K < ng) {  // uniform
       const int subs = (ng - 4 * K) < 4 ? (ng - 4 * K) : 4;
       for (int sub = 0; sub < subs - 1; ++sub) {  // next step in the same pivot block
-        sweep_mfma<NC, K, true>(M, a, b, TA);
+        sweep_mfma<NC, K, true, LDL, KM>(M, a, b, TA);
         sweep_diagfix<NC, K>(M, sub, g, c);
-        sweep_publish<NC, K>(s, M, sub + 1, g, c);
-        sweep_mfma<NC, K, false>(M, a, b, TA);
-        sweep_operands<NC>(s, 16 * K + 4 * (sub + 1), g, c, a, b);
+        sweep_publish<NC, K, LDL>(s, M, sub + 1, g, c);
+        sweep_mfma<NC, K, false, LDL, KM>(M, a, b, TA);
+        sweep_operands<NC, KM>(s, 16 * K + 4 * (sub + 1), g, c, a, b);
       }
       {  // last step of the block: the next step opens block K + 1
         const int sub = subs - 1;
         const bool has_next = 4 * (K + 1) < ng;
-        sweep_mfma<NC, K + 1, true>(M, a, b, TA);
+        sweep_mfma<NC, K + 1, true, LDL, KM>(M, a, b, TA);
         if constexpr (K + 1 < C::TT) {
-          if (has_next) sweep_publish<NC, K + 1>(s, M, 0, g, c);
+          if (has_next) sweep_publish<NC, K + 1, LDL>(s, M, 0, g, c);
         }
-        sweep_mfma<NC, K + 1, false>(M, a, b, TA);
+        sweep_mfma<NC, K + 1, false, LDL, KM>(M, a, b, TA);
         sweep_diagfix<NC, K>(M, sub, g, c);
-        if (has_next) sweep_operands<NC>(s, 16 * (K + 1), g, c, a, b);
+        if constexpr (K + 1 < C::TT) {
+          if (has_next) sweep_operands<NC, LDL ? K + 1 : 0>(s, 16 * (K + 1), g, c, a, b);
+        }
       }
     }
-    sweep_block<NC, K + 1>(s, M, ng, TA, g, c, a, b);
+    sweep_block<NC, K + 1, LDL>(s, M, ng, TA, g, c, a, b);
   }
 }
 
@@ -939,7 +952,14 @@ __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
 // ------------------------------------------------------------------------------------------
 // block sweep inversion (4 pivots per step, MFMA rank-4 updates)
 // ------------------------------------------------------------------------------------------
-template <int NC, class SM>
+// LDL = true: the same sweep restricted to the tiles right of the swept pivots -- a block LDL'
+// factorization (16-pivot blocks) instead of the inverse, at 4 T(TT - K) MFMAs per block K
+// instead of 4 NTL (T(m) = m (m + 1) / 2: 480 instead of 1,152 for NC = 128).  Sweeping block
+// K on rows / columns >= 16 K leaves -D_K^-1 in tile (K, K) (D_K the Schur-complemented pivot
+// block), L_IK = H_IK D_K^-1 in the tiles below it, and the Schur complement to its right;
+// unscaled, tile (K, K) holds D_K^-1 and tiles (I > J) the unit block-lower L of
+// H = L D L' (applied by ldl_apply).
+template <int NC, bool LDL = false, class SM>
 __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n) {
   using C = Cfg<NC>;
   const int lane = opaque_lane();
@@ -972,9 +992,9 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
   if constexpr (NC <= kSweepPipeMaxNC) {
     if (ng > 0) {
       float a[C::TT], b[C::TT];
-      sweep_publish<NC, 0>(s, M, 0, g, c);
-      sweep_operands<NC>(s, 0, g, c, a, b);
-      sweep_block<NC, 0>(s, M, ng, TA, g, c, a, b);
+      sweep_publish<NC, 0, LDL>(s, M, 0, g, c);
+      sweep_operands<NC, 0>(s, 0, g, c, a, b);
+      sweep_block<NC, 0, LDL>(s, M, ng, TA, g, c, a, b);
     }
   } else {
   const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
@@ -1004,7 +1024,7 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
           for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
         }
       }
-      if (roww) {
+      if (!LDL && roww) {
 #pragma unroll
         for (int J = 0; J < K; ++J)
           *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(K, J)];
@@ -1039,21 +1059,22 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
       const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
       const float w3 = g3 ? 1.f : 0.f;
       const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
+      const int KM = LDL ? K : 0;  // (a constant once the K loop is unrolled)
       f4 ph[C::TT];
 #pragma unroll
-      for (int I = 0; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
+      for (int I = KM; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
       float a[C::TT], b[C::TT];
 #pragma unroll
-      for (int I = 0; I < C::TT; ++I) {
+      for (int I = KM; I < C::TT; ++I) {
         const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
         a[I] = -yg;
         b[I] = yg * ig;
       }
 #pragma unroll
-      for (int I = 0; I < C::TT; ++I) {
+      for (int I = KM; I < C::TT; ++I) {
         if (I >= TA) continue;  // uniform
 #pragma unroll
-        for (int J = 0; J <= I; ++J) {
+        for (int J = KM; J <= I; ++J) {
           const int t = tile_index(I, J);
           M[t] = mfma4(a[I], b[J], M[t]);
         }
@@ -1066,18 +1087,95 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
     }
   }
   }
-  // M holds -(scaled inverse): undo sign and scaling
+  // M holds -(scaled inverse): undo sign and scaling (LDL: the diagonal tiles hold -(scaled
+  // D_K^-1), the tiles below them the scaled L~ = S^-1 L S)
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) {
     const f4 ri = *reinterpret_cast<const f4*>(&s.ds[16 * I + 4 * g]);
+    f4 rinv;
+    if constexpr (LDL) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) rinv[q] = 1.f / ri[q];
+    }
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
-      const float cj = -s.ds[16 * J + c];
+      const float cj = s.ds[16 * J + c];
       f4& m = M[tile_index(I, J)];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] *= ri[q] * cj;
+      for (int q = 0; q < 4; ++q) m[q] *= (LDL && J < I) ? rinv[q] * cj : -(ri[q] * cj);
     }
   }
+}
+
+// out = (L D L')^-1 in over the first n params (factors from invert_tiles<NC, true>; out is
+// zero beyond n): z = L^-1 in block row by block row (row sums over the block's columns), then
+// x = L'^-1 D^-1 z from the last block row up (column sums over the row's 4-lane groups); each
+// block's result turns layout (rows <-> columns) through `out`, which holds z, then x.
+template <int NC, class SM>
+__device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], int n,
+                                          const float* in, float* out) {
+  using C = Cfg<NC>;
+  CMPC_T0(t_sv);
+  const int lane = opaque_lane();
+  const int g = lane >> 4, c = lane & 15;
+  n = uniform(n);
+  const int TA = (n + 15) >> 4;
+  WSYNC();
+  float zc[C::TT];  // z by block, column layout (lane c: z[16 J + c])
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) {
+    if (I >= TA) {  // padding rows: zero (uniform branch)
+      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = f4{0.f, 0.f, 0.f, 0.f};
+      continue;
+    }
+    f4 zr = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
+    if (I > 0) {
+      f2 r01 = {0.f, 0.f}, r23 = {0.f, 0.f};
+#pragma unroll
+      for (int J = 0; J < I; ++J) {
+        const f4 m = M[tile_index(I, J)];
+        const f2 zj = {zc[J], zc[J]};
+        r01 = __builtin_elementwise_fma(f2{m[0], m[1]}, zj, r01);
+        r23 = __builtin_elementwise_fma(f2{m[2], m[3]}, zj, r23);
+      }
+      zr[0] -= row16_sum(r01[0]);
+      zr[1] -= row16_sum(r01[1]);
+      zr[2] -= row16_sum(r23[0]);
+      zr[3] -= row16_sum(r23[1]);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zr[q] = (16 * I + 4 * g + q < n) ? zr[q] : 0.f;
+    if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
+    WSYNC();
+    zc[I] = out[16 * I + c];
+  }
+  // backward: x_I = D_I^-1 z_I - sum_{J > I} L_JI' x_J, accumulated per lane (column layout
+  // after the 4-group sum) as each x_J is known
+  float bc[C::TT];
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) bc[I] = 0.f;
+#pragma unroll
+  for (int I = C::TT - 1; I >= 0; --I) {
+    if (I >= TA) continue;  // uniform
+    const f4 zr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
+    const f4 d = M[tile_index(I, I)];
+    const float t = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
+    float xc = col4_sum(t);
+    xc = (16 * I + c < n) ? xc : 0.f;
+    WSYNC();
+    if (g == 0) out[16 * I + c] = xc;
+    WSYNC();
+    if (I == 0) break;
+    const f4 xr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
+#pragma unroll
+    for (int J = 0; J < I; ++J) {
+      const f4 m = M[tile_index(I, J)];
+      bc[J] = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], fmaf(m[0], xr[0], bc[J]))));
+    }
+  }
+  WSYNC();
+  CMPC_ACC(3, t_sv);
+  CMPC_CNT(13, 1);
 }
 
 // out = M in over the first n params (M in register tiles, symmetric, lower triangle stored);
@@ -1462,7 +1560,8 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
 template <int NC, int NT>
 __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const f4 (&M)[NT], int n,
                                            const float* in, float* out) {
-  symv<NC>(s, M, n, in, out);
+  if constexpr (ldl_for<NC>()) ldl_apply<NC>(s, M, n, in, out);
+  else symv<NC>(s, M, n, in, out);
 }
 template <int NC>
 __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const RicRegs& F, int n,
@@ -2186,7 +2285,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         condense_tiles<NC>(s, P, M, nact, uniformf(shift), nil);
         CMPC_ACC(0, t_c);
         CMPC_T0(t_i);
-        invert_tiles<NC>(s, M, nact);
+        invert_tiles<NC, ldl_for<NC>()>(s, M, nact);
         CMPC_ACC(1, t_i);
       } else {
         CMPC_T0(t_c);

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Round 5: GPU tests + parity survey of the product library (ambiguity band 5 tol), the default
 # bench line (warm tail, 1,024-robot closed loop) with and without the one-wave-per-CU team
-# kernel, the Riccati variant's stamps/anatomy after the sweep restructure, A/B product vs
-# Riccati vs a capped NC192 grid.
+# kernel, A/B of the product vs the block-LDL' variant vs Riccati for the NC 192 bin (also on
+# standing batches), LDL' stamps, the NC 192 kernel's span with an empty bin.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 L=convex-mpc-unitree-go2_amd/cmpc/lib
@@ -23,15 +23,11 @@ for f in ("bench_default", "bench_occ1"):
           "warm itmax %s cold itmax %s warm p999 %s cold p999 %s" % (w.get("iters_max_warm"), w.get("iters_max_cold"), w.get("iters_p999_warm"), w.get("iters_p999_cold")),
           "loop1024 graph %.3f ms eager %.3f ms" % (cl.get("ms_per_tick_graph", -1), cl.get("ms_per_tick_eager", -1)))
 EOF
-for c in 1 2; do
-  timeout -k 10 120 python tools/stamps.py --config $c --batch 8192 --team 0 --lib $L/libcmpc_ric_stamps.so > gpurun_out/st_ric_stamps_cfg$c.txt 2>&1 || { tail -5 gpurun_out/st_ric_stamps_cfg$c.txt; exit 1; }
-  grep -E "==|per call|instance total|mean iters" gpurun_out/st_ric_stamps_cfg$c.txt
-done
-CMPC_DIAG_LIB=$L/libcmpc_ric_diag.so timeout -k 10 300 python tools/diag_counts.py > gpurun_out/dc_ric_diag.txt 2>&1 || { tail -5 gpurun_out/dc_ric_diag.txt; exit 1; }
-grep -E "^cfg|max:" gpurun_out/dc_ric_diag.txt
-TESTS=0 R=1 CASES="3:65536 2:4096" bash scripts/gpu_ab.sh $L/libcmpc.so $L/libcmpc_ric.so $L/libcmpc_ric192.so || exit 1
-# standing batches (every instance NC 192): explicit inverse vs Riccati for that bin
-BENCH_ARGS=--stance-all TESTS=0 R=1 CASES="2:4096 2:16384" bash scripts/gpu_ab.sh $L/libcmpc.so $L/libcmpc_ric192.so || exit 1
+TESTS=0 R=1 CASES="3:65536 2:4096" bash scripts/gpu_ab.sh $L/libcmpc.so $L/libcmpc_ldl.so $L/libcmpc_ric192.so || exit 1
+timeout -k 10 120 python tools/stamps.py --config 2 --batch 8192 --team 0 --lib $L/libcmpc_ldl_stamps.so > gpurun_out/st_ldl_stamps_cfg2.txt 2>&1 || { tail -5 gpurun_out/st_ldl_stamps_cfg2.txt; exit 1; }
+grep -E "==|per call|instance total|mean iters" gpurun_out/st_ldl_stamps_cfg2.txt
+# standing batches (every instance NC 192): explicit inverse vs LDL vs Riccati for that bin
+BENCH_ARGS=--stance-all TESTS=0 R=1 CASES="2:4096 2:16384" bash scripts/gpu_ab.sh $L/libcmpc.so $L/libcmpc_ldl.so $L/libcmpc_ric192.so || exit 1
 # the NC 192 kernel's span with an empty bin (config 1 at 65,536: no NC 192 instance)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/span -o run --output-format csv -- python bench.py --aux 0 --config 1 --batch 65536 --steps 5 --warmup 1 > gpurun_out/span.log 2>&1 || { tail -5 gpurun_out/span.log; exit 1; }
 echo done
