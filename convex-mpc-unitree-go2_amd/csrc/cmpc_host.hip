@@ -252,8 +252,12 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
+  // the NC 192 stream at the highest priority: its few early waves are dispatched ahead of the
+  // register classes submitted right after them on the other queues (solve_impl)
+  int prio_lo = 0, prio_hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) prio_hi = 0;
   if ((e = hipStreamCreateWithFlags(&pl->side, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipStreamCreateWithFlags(&pl->top, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithPriority(&pl->top, hipStreamNonBlocking, prio_hi)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->fork, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->join, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&pl->join_top, hipEventDisableTiming)) != hipSuccess) {

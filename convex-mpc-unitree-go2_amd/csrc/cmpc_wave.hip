@@ -54,9 +54,9 @@ constexpr bool ric_for() {
 }
 // The one-wave kernels of the bins with NC >= CMPC_LDL_MIN_NC keep a block LDL' factorization
 // of (H + shift I) in the register tiles instead of its inverse (invert_tiles<NC, true>,
-// ldl_apply); 0: none
+// ldl_apply); 0: none (the explicit inverse of rounds 1-4: -DCMPC_LDL_MIN_NC=0)
 #ifndef CMPC_LDL_MIN_NC
-#define CMPC_LDL_MIN_NC 0
+#define CMPC_LDL_MIN_NC 1
 #endif
 template <int NC>
 constexpr bool ldl_for() {
@@ -1060,13 +1060,11 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
       const float w3 = g3 ? 1.f : 0.f;
       const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
       const int KM = LDL ? K : 0;  // (a constant once the K loop is unrolled)
-      f4 ph[C::TT];
-#pragma unroll
-      for (int I = KM; I < C::TT; ++I) ph[I] = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
       float a[C::TT], b[C::TT];
 #pragma unroll
       for (int I = KM; I < C::TT; ++I) {
-        const float yg = fmaf(w3, ph[I][3], fmaf(w2, ph[I][2], fmaf(w1, ph[I][1], w0 * ph[I][0])));
+        const f4 ph = *reinterpret_cast<const f4*>(&s.pan[(16 * I + c) * 4]);
+        const float yg = fmaf(w3, ph[3], fmaf(w2, ph[2], fmaf(w1, ph[1], w0 * ph[0])));
         a[I] = -yg;
         b[I] = yg * ig;
       }
