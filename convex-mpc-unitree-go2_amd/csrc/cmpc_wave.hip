@@ -2298,7 +2298,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // kRefineExtra) while the step still contracts and is above the acceptance tolerance --
       // an ill-conditioned face set (internal foot forces weigh only R) contracts slowly
       float step = 3.0e38f, prev = 3.0e38f, vscale = 1.f;
-      bool ok = false, changed = false, loose = false, converged = false;
+      bool ok = false, changed = false, loose = false, converged = false, stalled = false;
       for (int pass = 0;; ++pass) {
         // (an extra pass -- ambiguous face multipliers, below -- is one more refinement step)
         for (int q = pass == 0 ? 0 : CMPC_REFINE_N + kRefineExtra - 1;
@@ -2324,9 +2324,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   #ifdef CMPC_TRACE
           if (b == CMPC_TRACE && lane == 0) printf("    refine %d step %g\n", q, step);
   #endif
-          if (q + 1 >= CMPC_REFINE_N &&
-              (step <= P.polish_tol * wave_max(mv) || step > kRefineRate * prev))
-            break;
+          stalled = step > kRefineRate * prev;
+          if (q + 1 >= CMPC_REFINE_N && (step <= P.polish_tol * wave_max(mv) || stalled)) break;
           prev = step;
         }
         gradient<NC, (W > 1), true>(s, P, nact, s.v, s.g, pwc, twc);  // E, L at the final point
@@ -2356,7 +2355,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
                nact, nadd, (int)ok, (int)loose, (int)changed, step, repairs_left);
 #endif
       CMPC_ACC(4, t_pol);
-      if (ok) {
+      // A refinement on a downdated inverse that stopped contracting above the tight level
+      // (fp32 downdates of an ill-conditioned face set: steps 1e-4, 3.1e-5, 2.9e-5) has no
+      // reliable multipliers -- config-3 instance 31861 held a degenerate friction face at
+      // -1.6e-7, released it, found it violated, and cycled through 5 sessions and 130 ADMM
+      // iterations: the face set is refactored exactly before the check decides anything.
+      const bool dd_stall = nadd > 0 && stalled && step > kAmbConverged * P.polish_tol * vscale;
+      if (dd_stall) converged = false;
+      if (ok && !dd_stall) {
         polished = true;
         status = 1;
         break;
