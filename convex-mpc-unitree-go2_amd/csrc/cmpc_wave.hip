@@ -58,6 +58,12 @@ constexpr bool ric_for() {
 #ifndef CMPC_LDL_MIN_NC
 #define CMPC_LDL_MIN_NC 1
 #endif
+// ldl_apply turns each block between the row and column layouts in registers (DPP / permlane
+// swaps) instead of through LDS
+#ifndef CMPC_APPLY_DPP
+#define CMPC_APPLY_DPP 1
+#endif
+constexpr bool kApplyDpp = CMPC_APPLY_DPP;
 template <int NC>
 constexpr bool ldl_for() {
   return !ric_for<NC>() && CMPC_LDL_MIN_NC > 0 && NC >= CMPC_LDL_MIN_NC;
@@ -159,6 +165,36 @@ __device__ __forceinline__ float col4_sum(float v) {
 
 // sum over the wave, result in every lane
 __device__ __forceinline__ float wave_sum(float v) { return col4_sum(row16_sum(v)); }
+
+// Layout turns of a 16-vector without LDS.  Rows layout: every lane of DPP row g holds
+// z[4g .. 4g+3] in its four registers; columns layout: every lane of column c (= lane & 15)
+// holds z[c].
+// rows -> columns: each lane picks z[4g + (c & 3)], then takes the pick of row c >> 2 in its own
+// column (one 16-lane and two 32-lane swaps give every lane its column's four rows)
+__device__ __forceinline__ float rows_to_cols(const f4& zr, int g, int c) {
+  const int q = c & 3;
+  const float t = q == 0 ? zr[0] : q == 1 ? zr[1] : q == 2 ? zr[2] : zr[3];
+  float a0, a1, r0, r2, r1, r3;
+  pair16(t, a0, a1);  // rows (g & 2) and (g & 2) | 1 of this column
+  pair32(a0, r0, r2);
+  pair32(a1, r1, r3);
+  const int src = c >> 2;
+  return src == 0 ? r0 : src == 1 ? r1 : src == 2 ? r2 : r3;
+}
+// columns -> rows: rotate row g right by 16 - 4g (row_ror with a row mask: rows 1, 3 by 12,
+// rows 2, 3 by 8), so lane q of row g holds z[4g + q]; then broadcast lanes 0..3 of each row
+// (row_newbcast)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_rows(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
+                                                    ROWS, 0xF, false));
+}
+__device__ __forceinline__ f4 cols_to_rows(float zc) {
+  float t = dpp_rows<0x12C, 0xA>(zc, zc);  // row_ror:12 on rows 1, 3
+  t = dpp_rows<0x128, 0xC>(t, t);          // row_ror:8 on rows 2, 3
+  return f4{dpp_rows<0x150, 0xF>(0.f, t), dpp_rows<0x151, 0xF>(0.f, t),
+            dpp_rows<0x152, 0xF>(0.f, t), dpp_rows<0x153, 0xF>(0.f, t)};
+}
 
 // Lane id the compiler cannot see as loop invariant: every phase re-derives its lane-dependent
 // addresses locally instead of the persistent loops hoisting them (and spilling them) for the
@@ -1120,6 +1156,11 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
   const int TA = (n + 15) >> 4;
   WSYNC();
   float zc[C::TT];  // z by block, column layout (lane c: z[16 J + c])
+  // backward accumulators (column layout, per lane before the 4-group sum): D_I^-1 z_I as the
+  // forward sweep finds z_I (register turns), then minus L_JI' x_J as each x_J is known
+  float bc[C::TT];
+#pragma unroll
+  for (int I = 0; I < C::TT; ++I) bc[I] = 0.f;
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) {
     if (I >= TA) {  // padding rows: zero (uniform branch)
@@ -1143,32 +1184,46 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) zr[q] = (16 * I + 4 * g + q < n) ? zr[q] : 0.f;
-    if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
-    WSYNC();
-    zc[I] = out[16 * I + c];
+    if constexpr (kApplyDpp) {
+      zc[I] = rows_to_cols(zr, g, c);
+      const f4 d = M[tile_index(I, I)];
+      bc[I] = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], d[0] * zr[0])));
+    } else {
+      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
+      WSYNC();
+      zc[I] = out[16 * I + c];
+    }
   }
-  // backward: x_I = D_I^-1 z_I - sum_{J > I} L_JI' x_J, accumulated per lane (column layout
-  // after the 4-group sum) as each x_J is known
-  float bc[C::TT];
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) bc[I] = 0.f;
+  // backward: x_I = D_I^-1 z_I - sum_{J > I} L_JI' x_J
 #pragma unroll
   for (int I = C::TT - 1; I >= 0; --I) {
     if (I >= TA) continue;  // uniform
-    const f4 zr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
-    const f4 d = M[tile_index(I, I)];
-    const float t = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
+    float t;
+    if constexpr (kApplyDpp) {
+      t = bc[I];
+    } else {
+      const f4 zr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
+      const f4 d = M[tile_index(I, I)];
+      t = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
+    }
     float xc = col4_sum(t);
     xc = (16 * I + c < n) ? xc : 0.f;
     WSYNC();
     if (g == 0) out[16 * I + c] = xc;
-    WSYNC();
     if (I == 0) break;
-    const f4 xr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
+    f4 xr;
+    if constexpr (kApplyDpp) {
+      xr = cols_to_rows(xc);
+    } else {
+      WSYNC();
+      xr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
+    }
+    const float sg = kApplyDpp ? -1.f : 1.f;
 #pragma unroll
     for (int J = 0; J < I; ++J) {
       const f4 m = M[tile_index(I, J)];
-      bc[J] = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], fmaf(m[0], xr[0], bc[J]))));
+      const float u = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], m[0] * xr[0])));
+      bc[J] = fmaf(sg, u, bc[J]);
     }
   }
   WSYNC();
@@ -1746,7 +1801,8 @@ template <int NC>
 __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
                                              const float* __restrict__ Bg, int ntri, float step,
                                              bool& changed, bool& loose, bool& converged,
-                                             bool& amb, int top = 0, bool tr = false) {
+                                             bool& amb, bool& decisive, int top = 0,
+                                             bool tr = false) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
   float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -1800,7 +1856,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     tfy = fminf(tol_d, fe * s.R2[3 * leg + 1]);
     tfz = fminf(tol_d, fe * s.R2[3 * leg + 2]);
   }
-  bool ok = true, am = false;
+  bool ok = true, am = false, dec = false;
   int nc = 0;
   float v = 0.f;
   if (owns) {
@@ -1814,13 +1870,13 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     const float ta = kAmbBand * tol_d;
     am = prec && ((sx && lx < ta) || (sy && ly < ta) || (zl && l0 < ta));
     nc = code;
-    if (sx && lx < -tfx) { ok = false; nc &= ~6; }
-    if (sy && ly < -tfy) { ok = false; nc &= ~24; }
-    if (zl && l0 < -tfz) { ok = false; nc &= ~1; }
-    if (!sx && fabsf(fx) > mu * fz + tol_p) { ok = false; nc |= (fx > 0.f) ? 2 : 4; }
-    if (!sy && fabsf(fy) > mu * fz + tol_p) { ok = false; nc |= (fy > 0.f) ? 8 : 16; }
-    if (!zl && fz < fzmin - tol_p) { ok = false; nc |= 1; }
-    if (!(isfinite(fx) && isfinite(fy) && isfinite(fz))) ok = false;
+    if (sx && lx < -tfx) { ok = false; nc &= ~6; dec = dec || lx < -ta; }
+    if (sy && ly < -tfy) { ok = false; nc &= ~24; dec = dec || ly < -ta; }
+    if (zl && l0 < -tfz) { ok = false; nc &= ~1; dec = dec || l0 < -ta; }
+    if (!sx && fabsf(fx) > mu * fz + tol_p) { ok = false; nc |= (fx > 0.f) ? 2 : 4; dec = true; }
+    if (!sy && fabsf(fy) > mu * fz + tol_p) { ok = false; nc |= (fy > 0.f) ? 8 : 16; dec = true; }
+    if (!zl && fz < fzmin - tol_p) { ok = false; nc |= 1; dec = true; }
+    if (!(isfinite(fx) && isfinite(fy) && isfinite(fz))) { ok = false; dec = true; }
     const float ig = 1.f / fmaxf(gs, 1e-30f), iu = 1.f / us;
     v = fmaxf(fmaxf(sx ? -lx * ig : 0.f, sy ? -ly * ig : 0.f), zl ? -l0 * ig : 0.f);
     v = fmaxf(v, fmaxf(sx ? 0.f : (fabsf(fx) - mu * fz) * iu, sy ? 0.f : (fabsf(fy) - mu * fz) * iu));
@@ -1860,6 +1916,8 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   if (owns) s.tcnt[lane] = nc;  // repaired code (copied into s.code by the caller if used)
   changed = __any(owns && nc != code) != 0;
   amb = __any(am) != 0;
+  // (only multipliers within the ambiguity band fail: the decision rests on the point's accuracy)
+  decisive = __any(dec) != 0;
   const bool step_ok = step <= P.polish_tol * us;
   converged = step_ok;
   loose = (__all(lok) != 0) && step_ok;
@@ -2299,6 +2357,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // an ill-conditioned face set (internal foot forces weigh only R) contracts slowly
       float step = 3.0e38f, prev = 3.0e38f, vscale = 1.f;
       bool ok = false, changed = false, loose = false, converged = false, stalled = false;
+      bool decisive = true;
       for (int pass = 0;; ++pass) {
         // (an extra pass -- ambiguous face multipliers, below -- is one more refinement step)
         for (int q = pass == 0 ? 0 : CMPC_REFINE_N + kRefineExtra - 1;
@@ -2334,10 +2393,11 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         const int top = (kRepairTop > 0 && (nfail > 0 || ntried >= 3)) ? kRepairTop : 0;
         bool amb = false;
   #ifdef CMPC_TRACE
-        ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, top,
-                              b == CMPC_TRACE);
+        ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
+                              top, b == CMPC_TRACE);
   #else
-        ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, top);
+        ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
+                              top);
   #endif
         // A face multiplier near zero decides the check but moves by ~|H| x the point's remaining
         // error (a step accepted at polish_tol x the force scale leaves ~1e-5 N, i.e. ~1e-7 in a
@@ -2356,13 +2416,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #endif
       CMPC_ACC(4, t_pol);
       // A refinement on a downdated inverse that stopped contracting above the tight level
-      // (fp32 downdates of an ill-conditioned face set: steps 1e-4, 3.1e-5, 2.9e-5) has no
-      // reliable multipliers -- config-3 instance 31861 held a degenerate friction face at
-      // -1.6e-7, released it, found it violated, and cycled through 5 sessions and 130 ADMM
-      // iterations: the face set is refactored exactly before the check decides anything.
-      const bool dd_stall = nadd > 0 && stalled && step > kAmbConverged * P.polish_tol * vscale;
+      // (fp32 downdates of an ill-conditioned face set: steps 1e-4, 3.1e-5, 2.9e-5) leaves
+      // multipliers near zero unreliable -- config-3 instance 31861 held a degenerate friction
+      // face at -1.6e-7, released it, found it violated, and cycled through 5 sessions and 130
+      // ADMM iterations.  When only such multipliers fail the check, the face set is refactored
+      // exactly before the check decides.  (Refactoring every stalled downdate also fixed 31861
+      // but cost 6-10 % more factorizations on configs 2-3: most stalls sit at the fp32 floor
+      // of checks that large violations decide anyway.)
+      const bool dd_stall = nadd > 0 && stalled && !ok && !decisive &&
+                            step > kAmbConverged * P.polish_tol * vscale;
       if (dd_stall) converged = false;
-      if (ok && !dd_stall) {
+      if (ok) {
         polished = true;
         status = 1;
         break;

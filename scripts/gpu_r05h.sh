@@ -22,4 +22,17 @@ TESTS=0 R=2 CASES="3:65536 2:4096 2:65536" bash scripts/gpu_ab.sh $L/libcmpc.so 
 timeout -k 10 300 python -u tests/certify_sample.py gpu > gpurun_out/survey_gpu.log 2>&1 || { tail -5 gpurun_out/survey_gpu.log; exit 1; }
 timeout -k 10 600 python -u tests/certify_sample.py cpu > gpurun_out/survey_cpu.log 2>&1 || { tail -5 gpurun_out/survey_cpu.log; exit 1; }
 grep -E "above 1e-4|^cfg" gpurun_out/survey_cpu.log
+# small batches: the team kernel's two-per-CU image (B 257..1,024) vs the one-wave kernels
+for cb in 2:512 2:1024 3:1024 1:1024; do
+  cfg=${cb%%:*}; B=${cb##*:}
+  for t in -1 256; do
+    timeout -k 10 120 python bench.py --aux 0 --config $cfg --batch $B --steps 20 --team $t > gpurun_out/tm_${cfg}_${B}_$t.json 2> gpurun_out/tm.err || { tail -5 gpurun_out/tm.err; exit 1; }
+    python -c "import json;a=json.load(open('gpurun_out/tm_${cfg}_${B}_$t.json'));print('cfg $cfg B $B team $t: %.3f ms itmax %d'%(a['ms_per_step'],a['iters_max']))"
+  done
+done
+LOOP="--sub-configs 0 --dynamics-steps 0 --tick-steps 0 --leg-steps 0 --api-ticks 0 --warm-steps 0 --cpu-seconds 1"
+for t in -1 256; do
+  timeout -k 10 300 python bench.py $LOOP --team $t > gpurun_out/loop_$t.json 2> gpurun_out/loop.err || { tail -5 gpurun_out/loop.err; exit 1; }
+  python -c "import json;a=json.loads(open('gpurun_out/loop_$t.json').read().strip().splitlines()[-1]);c=a['closed_loop']['robots_1024'];print('loop 1024 team $t: graph %.3f ms eager %.3f ms'%(c['ms_per_tick_graph'],c['ms_per_tick_eager']))"
+done
 echo done
