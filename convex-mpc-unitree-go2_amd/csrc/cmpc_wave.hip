@@ -352,6 +352,9 @@ constexpr bool kWarmRestart = CMPC_WARM_RESTART;
 #endif
 constexpr float kFaceErr = CMPC_FACE_ERR;
 constexpr float kLooseFace = 2.5f;
+// a downdated refinement that stopped contracting accepts nothing while its step is above
+// kStallAccept x the acceptance tolerance (the face set is refactored first)
+constexpr float kStallAccept = 0.1f;
 // A check decided by a face multiplier within polish_tol x gs of zero is repeated after up to
 // kAmbRefine more refinement steps (unless the step is already below kAmbConverged x the
 // acceptance tolerance)
@@ -2423,8 +2426,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // exactly before the check decides.  (Refactoring every stalled downdate also fixed 31861
       // but cost 6-10 % more factorizations on configs 2-3: most stalls sit at the fp32 floor
       // of checks that large violations decide anyway.)
-      const bool dd_stall = nadd > 0 && stalled && !ok && !decisive &&
-                            step > kAmbConverged * P.polish_tol * vscale;
+      // Nor is a point accepted while a downdated refinement stopped contracting at more than
+      // a tenth of the acceptance tolerance: the step is then no bound on the point's error
+      // (config-3 instance 39503 under the light-bin schedule: three downdates, steps 2.2e-4,
+      // 5.7e-4, 5.0e-4 against a tolerance of 9.7e-4, accepted 0.037 N = 3.8e-4 off).
+      const bool dd_stall =
+          nadd > 0 && stalled &&
+          ((!ok && !decisive && step > kAmbConverged * P.polish_tol * vscale) ||
+           step > kStallAccept * P.polish_tol * vscale);
       if (dd_stall) converged = false;
       if (ok) {
         polished = true;
