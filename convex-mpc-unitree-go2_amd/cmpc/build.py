@@ -11,7 +11,7 @@ REPO = ROOT.parent
 CSRC = ROOT / "csrc"
 LIB = PKG / "lib" / "libcmpc.so"
 SOURCES = [CSRC / "cmpc_host.hip"]
-DEPS = SOURCES + [CSRC / "cmpc_wave.hip", CSRC / "cmpc_team.hip", CSRC / "cmpc_riccati.hip", CSRC / "cmpc_dynamics.hip", CSRC / "cmpc_traj.hip", CSRC / "cmpc_leg.hip", CSRC / "cmpc_sim.hip", CSRC / "cmpc_device.h", REPO / "include" / "cmpc.h"]
+DEPS = SOURCES + [CSRC / "cmpc_wave.hip", CSRC / "cmpc_team.hip", CSRC / "cmpc_dynamics.hip", CSRC / "cmpc_traj.hip", CSRC / "cmpc_leg.hip", CSRC / "cmpc_sim.hip", CSRC / "cmpc_device.h", REPO / "include" / "cmpc.h"]
 ARCH = os.environ.get("CMPC_OFFLOAD_ARCH", "gfx950")
 
 

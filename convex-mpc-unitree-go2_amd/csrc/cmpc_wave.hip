@@ -33,25 +33,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
 
 #include "cmpc_device.h"
 
 namespace cmpc {
 
-// The one-wave kernels factor (H + shift I) by the Riccati recursion of the horizon
-// (cmpc_riccati.hip) instead of condensing and inverting it in register tiles
-#ifndef CMPC_RICCATI
-#define CMPC_RICCATI 0
-#endif
-// ... or only the bins with NC >= CMPC_RICCATI_MIN_NC (0: none)
-#ifndef CMPC_RICCATI_MIN_NC
-#define CMPC_RICCATI_MIN_NC 0
-#endif
-template <int NC>
-constexpr bool ric_for() {
-  return CMPC_RICCATI || (CMPC_RICCATI_MIN_NC > 0 && NC >= CMPC_RICCATI_MIN_NC);
-}
 // The one-wave kernels of the bins with NC >= CMPC_LDL_MIN_NC keep a block LDL' factorization
 // of (H + shift I) in the register tiles instead of its inverse (invert_tiles<NC, true>,
 // ldl_apply); 0: none (the explicit inverse of rounds 1-4: -DCMPC_LDL_MIN_NC=0)
@@ -66,7 +52,7 @@ constexpr bool ric_for() {
 constexpr bool kApplyDpp = CMPC_APPLY_DPP;
 template <int NC>
 constexpr bool ldl_for() {
-  return !ric_for<NC>() && CMPC_LDL_MIN_NC > 0 && NC >= CMPC_LDL_MIN_NC;
+  return CMPC_LDL_MIN_NC > 0 && NC >= CMPC_LDL_MIN_NC;
 }
 
 #ifndef CMPC_WPE_OVERRIDE
@@ -257,8 +243,8 @@ struct Cfg {
   static constexpr int TT = NC / 16;             // 16x16 tile rows
   static constexpr int NTL = TT * (TT + 1) / 2;  // lower-triangle tiles (f4 per lane each)
   static constexpr int THREADS = 64;             // one wave per QP
-  // per wave (floats): park slab of the inverse (or of the Riccati factors: 144 per lane)
-  static constexpr int SLAB = (ric_for<NC>() && NTL * 256 < 144 * 64) ? 144 * 64 : NTL * 256;
+  // per wave (floats): park slab of the register tiles (inverse or LDL' factors)
+  static constexpr int SLAB = NTL * 256;
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
   static constexpr int WPE = CMPC_WPE_OVERRIDE;
 };
@@ -352,9 +338,6 @@ constexpr bool kWarmRestart = CMPC_WARM_RESTART;
 #endif
 constexpr float kFaceErr = CMPC_FACE_ERR;
 constexpr float kLooseFace = 2.5f;
-// a downdated refinement that stopped contracting accepts nothing while its step is above
-// kStallAccept x the acceptance tolerance (the face set is refactored first)
-constexpr float kStallAccept = 0.1f;
 // A check decided by a face multiplier within polish_tol x gs of zero is repeated after up to
 // kAmbRefine more refinement steps (unless the step is already below kAmbConverged x the
 // acceptance tolerance)
@@ -1609,22 +1592,12 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
   CMPC_CNT(12, 1);
 }
 
-#include "cmpc_riccati.hip"  // (H + shift I)^-1 as a Riccati factorization (ric_for)
-
-// M applied to a param vector: the register-tile inverse, or the Riccati sweeps (which clobber
-// `in`)
+// M applied to a param vector: the LDL' solve or the register-tile inverse
 template <int NC, int NT>
 __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const f4 (&M)[NT], int n,
                                            const float* in, float* out) {
   if constexpr (ldl_for<NC>()) ldl_apply<NC>(s, M, n, in, out);
   else symv<NC>(s, M, n, in, out);
-}
-template <int NC>
-__device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const RicRegs& F, int n,
-                                           const float* in, float* out) {
-  // (every caller's `in` is dead after the apply: the ADMM right-hand side s.r, the
-  // refinement's gradient s.g, a downdate's face vector s.r)
-  ric_apply<NC>(s, P.N, F, n, const_cast<float*>(in), out);
 }
 
 // Euclidean projection of (a, b, c) onto {|x| <= mu z, |y| <= mu z, z >= fz_min}.
@@ -2084,15 +2057,6 @@ __device__ __forceinline__ void park_store(float* __restrict__ park, const f4 (&
 }
 
 template <int NC>
-__device__ __forceinline__ void park_store(float* __restrict__ park, const RicRegs& F) {
-  ric_park_store(park, F);
-}
-template <int NC>
-__device__ __forceinline__ void park_load(const float* __restrict__ park, RicRegs& F) {
-  ric_park_load(park, F);
-}
-
-template <int NC>
 __device__ __forceinline__ void park_load(const float* __restrict__ park, f4 (&M)[Cfg<NC>::NTL]) {
   const int lane = opaque_lane();
   asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc1" ::: "memory");
@@ -2151,11 +2115,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
                                                const Inputs& in, const Outputs& out,
                                                float* __restrict__ park, TeamSmem<NC, W>* ts,
                                                int* seq) {
-  // W = 1: the whole lower triangle in this wave's registers (or the Riccati factors);
-  // W > 1: this wave's team slots
-  using MinvT = typename std::conditional<(W == 1 && ric_for<NC>()), RicRegs,
-                                          f4[TeamCfg<NC, W>::SLOTS]>::type;
-  MinvT M;
+  // W = 1: the whole lower triangle in this wave's registers; W > 1: this wave's team slots
+  f4 M[TeamCfg<NC, W>::SLOTS];
   static_assert(W > 1 || TeamCfg<NC, W>::SLOTS == Cfg<NC>::NTL, "W = 1 holds every tile");
   const int lane = opaque_lane();
   const int N = P.N;
@@ -2335,11 +2296,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #ifdef CMPC_DIAG_COUNTS
       ++dg_fact;
 #endif
-      if constexpr (W == 1 && ric_for<NC>()) {
-        CMPC_T0(t_c);
-        ric_factor<NC>(s, P, M, nact, uniformf(shift));
-        CMPC_ACC(0, t_c);
-      } else if constexpr (W == 1) {
+      if constexpr (W == 1) {
         CMPC_T0(t_c);
         condense_tiles<NC>(s, P, M, nact, uniformf(shift), nil);
         CMPC_ACC(0, t_c);
@@ -2426,16 +2383,15 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // exactly before the check decides.  (Refactoring every stalled downdate also fixed 31861
       // but cost 6-10 % more factorizations on configs 2-3: most stalls sit at the fp32 floor
       // of checks that large violations decide anyway.)
-      // Nor is a point accepted while a downdated refinement stopped contracting at more than
-      // a tenth of the acceptance tolerance: the step is then no bound on the point's error
-      // (config-3 instance 39503 under the light-bin schedule: three downdates, steps 2.2e-4,
-      // 5.7e-4, 5.0e-4 against a tolerance of 9.7e-4, accepted 0.037 N = 3.8e-4 off).
-      const bool dd_stall =
-          nadd > 0 && stalled &&
-          ((!ok && !decisive && step > kAmbConverged * P.polish_tol * vscale) ||
-           step > kStallAccept * P.polish_tol * vscale);
+      // Nor is a point accepted while a downdated refinement stopped contracting above the
+      // fp32 floor: the step is then no bound on the point's error (config-3 instance 39503:
+      // three downdates, steps 2.2e-4, 5.7e-4, 5.0e-4 against a tolerance of 9.7e-4, accepted
+      // 0.037 N = 3.8e-4 off; 25651: one downdate, steps 6.8e-5, 4.3e-5, 1.0e-4, 2.0e-4 off).
+      const bool dd_stall = nadd > 0 && stalled &&
+                            step > kAmbConverged * P.polish_tol * vscale &&
+                            (ok || loose || !decisive);
       if (dd_stall) converged = false;
-      if (ok) {
+      if (ok && !dd_stall) {
         polished = true;
         status = 1;
         break;

@@ -20,5 +20,9 @@ for v in libcmpc libcmpc_lsd; do
   timeout -k 10 300 python -u tools/shard_times.py $L/$v.so 5 > gpurun_out/shard_$v.log 2>&1 || { tail -5 gpurun_out/shard_$v.log; exit 1; }
   echo "== $v"; cat gpurun_out/shard_$v.log | grep N=
 done
+for i in 39503 25651; do
+  timeout -k 10 120 python -u tools/trace_instance.py $i 3 > gpurun_out/trace_cfg3_$i.txt 2>&1 || { tail -5 gpurun_out/trace_cfg3_$i.txt; exit 1; }
+  tail -2 gpurun_out/trace_cfg3_$i.txt
+done
 TESTS=0 R=2 CASES="3:65536 2:4096 2:65536" bash scripts/gpu_ab.sh $L/libcmpc.so $L/libcmpc_prev.so $L/libcmpc_lsd.so || exit 1
 echo done
