@@ -44,10 +44,12 @@ namespace cmpc {
 #ifndef CMPC_LDL_MIN_NC
 #define CMPC_LDL_MIN_NC 1
 #endif
-// ldl_apply turns each block between the row and column layouts in registers (DPP / permlane
-// swaps) instead of through LDS
+// 1: ldl_apply turns each block between the row and column layouts in registers (DPP / permlane
+// swaps) instead of through LDS -- 2 % faster on config 3, but its arithmetic (the D^-1 products
+// summed in another order) drew status-1 answers up to 2e-4 off in the next-tick survey that the
+// LDS-turn build passes; 0 (default): through LDS
 #ifndef CMPC_APPLY_DPP
-#define CMPC_APPLY_DPP 1
+#define CMPC_APPLY_DPP 0
 #endif
 constexpr bool kApplyDpp = CMPC_APPLY_DPP;
 template <int NC>
@@ -338,6 +340,13 @@ constexpr bool kWarmRestart = CMPC_WARM_RESTART;
 #endif
 constexpr float kFaceErr = CMPC_FACE_ERR;
 constexpr float kLooseFace = 2.5f;
+// 1: nothing is accepted on a downdated refinement that stalled above the fp32 floor (the face
+// set is refactored first); 0 (default): only a check that ambiguous multipliers alone fail
+// refactors.  Both survey clean on this build; the guard costs 4 % on config 3.
+#ifndef CMPC_STALL_GUARD
+#define CMPC_STALL_GUARD 0
+#endif
+constexpr bool kStallGuard = CMPC_STALL_GUARD;
 // A check decided by a face multiplier within polish_tol x gs of zero is repeated after up to
 // kAmbRefine more refinement steps (unless the step is already below kAmbConverged x the
 // acceptance tolerance)
@@ -1204,12 +1213,15 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
       WSYNC();
       xr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
     }
-    const float sg = kApplyDpp ? -1.f : 1.f;
 #pragma unroll
     for (int J = 0; J < I; ++J) {
       const f4 m = M[tile_index(I, J)];
-      const float u = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], m[0] * xr[0])));
-      bc[J] = fmaf(sg, u, bc[J]);
+      if constexpr (kApplyDpp) {
+        const float u = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], m[0] * xr[0])));
+        bc[J] -= u;
+      } else {
+        bc[J] = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], fmaf(m[0], xr[0], bc[J]))));
+      }
     }
   }
   WSYNC();
@@ -2389,7 +2401,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // 0.037 N = 3.8e-4 off; 25651: one downdate, steps 6.8e-5, 4.3e-5, 1.0e-4, 2.0e-4 off).
       const bool dd_stall = nadd > 0 && stalled &&
                             step > kAmbConverged * P.polish_tol * vscale &&
-                            (ok || loose || !decisive);
+                            ((kStallGuard && (ok || loose)) || (!ok && !decisive));
       if (dd_stall) converged = false;
       if (ok && !dd_stall) {
         polished = true;
