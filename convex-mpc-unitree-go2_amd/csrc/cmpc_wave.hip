@@ -44,14 +44,19 @@ namespace cmpc {
 #ifndef CMPC_LDL_MIN_NC
 #define CMPC_LDL_MIN_NC 1
 #endif
-// 1: ldl_apply turns each block between the row and column layouts in registers (DPP / permlane
-// swaps) instead of through LDS -- 2 % faster on config 3, but its arithmetic (the D^-1 products
-// summed in another order) drew status-1 answers up to 2e-4 off in the next-tick survey that the
-// LDS-turn build passes; 0 (default): through LDS
+// How ldl_apply turns each block between the row and column layouts:
+//  0: through LDS (write, read back);
+//  1: in registers (DPP / permlane swaps), the D^-1 products formed in the forward sweep -- 2 %
+//     faster on config 3, but its sums run in another order, and with that arithmetic the
+//     next-tick survey drew status-1 answers up to 2e-4 off that the LDS build passes;
+//  2 (default): in registers, with exactly mode 0's arithmetic (bit-identical results: the
+//     turned values are copies; the backward sweep's z rows are read from LDS one block ahead,
+//     off the dependency chain)
 #ifndef CMPC_APPLY_DPP
-#define CMPC_APPLY_DPP 0
+#define CMPC_APPLY_DPP 2
 #endif
-constexpr bool kApplyDpp = CMPC_APPLY_DPP;
+constexpr int kApplyMode = CMPC_APPLY_DPP;
+constexpr bool kApplyDpp = kApplyMode == 1;
 template <int NC>
 constexpr bool ldl_for() {
   return CMPC_LDL_MIN_NC > 0 && NC >= CMPC_LDL_MIN_NC;
@@ -1179,10 +1184,13 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) zr[q] = (16 * I + 4 * g + q < n) ? zr[q] : 0.f;
-    if constexpr (kApplyDpp) {
+    if constexpr (kApplyMode == 1) {
       zc[I] = rows_to_cols(zr, g, c);
       const f4 d = M[tile_index(I, I)];
       bc[I] = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], d[0] * zr[0])));
+    } else if constexpr (kApplyMode == 2) {
+      zc[I] = rows_to_cols(zr, g, c);
+      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
     } else {
       if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
       WSYNC();
@@ -1190,12 +1198,19 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
     }
   }
   // backward: x_I = D_I^-1 z_I - sum_{J > I} L_JI' x_J
+  f4 zpre = {0.f, 0.f, 0.f, 0.f};  // (mode 2: block I's z rows, read during block I + 1)
+  WSYNC();
 #pragma unroll
   for (int I = C::TT - 1; I >= 0; --I) {
     if (I >= TA) continue;  // uniform
     float t;
-    if constexpr (kApplyDpp) {
+    if constexpr (kApplyMode == 1) {
       t = bc[I];
+    } else if constexpr (kApplyMode == 2) {
+      const f4 zr = (I == TA - 1) ? *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]) : zpre;
+      if (I > 0) zpre = *reinterpret_cast<const f4*>(&out[16 * (I - 1) + 4 * g]);
+      const f4 d = M[tile_index(I, I)];
+      t = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
     } else {
       const f4 zr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
       const f4 d = M[tile_index(I, I)];
@@ -1207,7 +1222,7 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
     if (g == 0) out[16 * I + c] = xc;
     if (I == 0) break;
     f4 xr;
-    if constexpr (kApplyDpp) {
+    if constexpr (kApplyMode != 0) {
       xr = cols_to_rows(xc);
     } else {
       WSYNC();
