@@ -49,11 +49,12 @@ namespace cmpc {
 //  1: in registers (DPP / permlane swaps), the D^-1 products formed in the forward sweep -- 2 %
 //     faster on config 3, but its sums run in another order, and with that arithmetic the
 //     next-tick survey drew status-1 answers up to 2e-4 off that the LDS build passes;
-//  2 (default): in registers, with exactly mode 0's arithmetic (bit-identical results: the
-//     turned values are copies; the backward sweep's z rows are read from LDS one block ahead,
-//     off the dependency chain)
+//  2: in registers, with exactly mode 0's arithmetic (bit-identical results: the turned values
+//     are copies; the backward sweep's z rows are read from LDS one block ahead) -- measured
+//     1.3 % slower than mode 0 on config 3 (profiles/r05n_gpu_call.txt);
+//  0 (default): through LDS
 #ifndef CMPC_APPLY_DPP
-#define CMPC_APPLY_DPP 2
+#define CMPC_APPLY_DPP 0
 #endif
 constexpr int kApplyMode = CMPC_APPLY_DPP;
 constexpr bool kApplyDpp = kApplyMode == 1;
@@ -1199,7 +1200,7 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
   }
   // backward: x_I = D_I^-1 z_I - sum_{J > I} L_JI' x_J
   f4 zpre = {0.f, 0.f, 0.f, 0.f};  // (mode 2: block I's z rows, read during block I + 1)
-  WSYNC();
+  if constexpr (kApplyMode == 2) WSYNC();
 #pragma unroll
   for (int I = C::TT - 1; I >= 0; --I) {
     if (I >= TA) continue;  // uniform
