@@ -346,6 +346,16 @@ constexpr bool kWarmRestart = CMPC_WARM_RESTART;
 #endif
 constexpr float kFaceErr = CMPC_FACE_ERR;
 constexpr float kLooseFace = 2.5f;
+// polish sessions: give up after CMPC_ABANDON_AFTER repairs whose face set still violates the KKT
+// conditions by more than kAbandonV (relative); 0: never
+#ifndef CMPC_ABANDON_AFTER
+#define CMPC_ABANDON_AFTER 0
+#endif
+constexpr int kAbandonAfter = CMPC_ABANDON_AFTER;
+#ifndef CMPC_ABANDON_V
+#define CMPC_ABANDON_V 1e-2f
+#endif
+constexpr float kAbandonV = CMPC_ABANDON_V;
 // 1: nothing is accepted on a downdated refinement that stalled above the fp32 floor (the face
 // set is refactored first); 0 (default): only a check that ambiguous multipliers alone fail
 // refactors.  Both survey clean on this build; the guard costs 4 % on config 3.
@@ -1805,8 +1815,8 @@ template <int NC>
 __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
                                              const float* __restrict__ Bg, int ntri, float step,
                                              bool& changed, bool& loose, bool& converged,
-                                             bool& amb, bool& decisive, int top = 0,
-                                             bool tr = false) {
+                                             bool& amb, bool& decisive, float& vworst,
+                                             int top = 0, bool tr = false) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
   float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -1922,6 +1932,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   amb = __any(am) != 0;
   // (only multipliers within the ambiguity band fail: the decision rests on the point's accuracy)
   decisive = __any(dec) != 0;
+  vworst = wave_max((owns && isfinite(v)) ? v : (owns ? 1e30f : 0.f));
   const bool step_ok = step <= P.polish_tol * us;
   converged = step_ok;
   loose = (__all(lok) != 0) && step_ok;
@@ -2346,6 +2357,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       float step = 3.0e38f, prev = 3.0e38f, vscale = 1.f;
       bool ok = false, changed = false, loose = false, converged = false, stalled = false;
       bool decisive = true;
+      float vworst = 0.f;
       for (int pass = 0;; ++pass) {
         // (an extra pass -- ambiguous face multipliers, below -- is one more refinement step)
         for (int q = pass == 0 ? 0 : CMPC_REFINE_N + kRefineExtra - 1;
@@ -2382,10 +2394,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         bool amb = false;
   #ifdef CMPC_TRACE
         ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
-                              top, b == CMPC_TRACE);
+                              vworst, top, b == CMPC_TRACE);
   #else
         ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
-                              top);
+                              vworst, top);
   #endif
         // A face multiplier near zero decides the check but moves by ~|H| x the point's remaining
         // error (a step accepted at polish_tol x the force scale leaves ~1e-5 N, i.e. ~1e-7 in a
@@ -2433,7 +2445,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         refactor = true;
         continue;
       }
-      if (repairs_left > 0 && changed && !tried_before<NC>(s, ntri, ntried)) {
+      // a session whose face sets are still far off after kAbandonAfter repairs is given up
+      // (back to ADMM) instead of spending its remaining repairs on them
+      const bool hopeless = kAbandonAfter > 0 && ntried > kAbandonAfter && vworst > kAbandonV;
+      if (repairs_left > 0 && changed && !hopeless && !tried_before<NC>(s, ntri, ntried)) {
         // re-polish on the repaired face set
         --repairs_left;
         bool dd = false;
