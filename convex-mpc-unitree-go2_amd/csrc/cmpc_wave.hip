@@ -2160,6 +2160,20 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   const int lane = opaque_lane();
   const int N = P.N;
   const int NP = 12 * N;
+#if defined(CMPC_POISON_LDS)  // diagnostic: NaN into the float scratch before every instance
+  if constexpr (W == 1) {
+    const float qn = __int_as_float(0x7fc00000);
+    for (int i = lane; i < 12 * NC; i += 64) s.G[i] = qn;
+    for (int i = lane; i < NC; i += 64) s.v[i] = qn;
+    WSYNC();
+  }
+#endif
+#if defined(CMPC_POISON_PARK)  // diagnostic: NaN into the wave's park slab before every instance
+  if constexpr (W == 1) {
+    const float qn = __int_as_float(0x7fc00000);
+    for (int i = lane; i < Cfg<NC>::SLAB; i += 64) park[i] = qn;
+  }
+#endif
   const float* Ab = in.Ad + b * 144;
   const float* Bg = in.Bd + b * (int64_t)N * 144;
   const float* gdb = in.gd + b * 12;
