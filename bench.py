@@ -394,11 +394,16 @@ def main(argv=None):
         step()
     sync()
     plan.timing_read()
+    plan.stats(reset=True)
     plan.set_timing(True)
     elapsed = timed_steps(step, args.steps, 0, sync, barrier, reduce_max)
     plan.set_timing(False)
     ms_k, calls_k = plan.timing_read()
+    acc = plan.stats(reset=True)   # (after the timed region: it synchronises)
     n_ranks = reduce_sum_int(1)
+    # acceptance statistics of the timed steps, summed over the ranks, per step (cmpc_plan_stats)
+    acceptance = {k: (reduce_sum_int(v) / args.steps if v is not None else None)
+                  for k, v in acc.items()}
     solved = reduce_sum_int(int((st == 1).sum().item()))
     status = st.cpu().numpy()
     iters = it.cpu().numpy()
@@ -541,6 +546,7 @@ def main(argv=None):
             "iters_mean": float(np.mean(iters)),
             "iters_max": int(np.max(iters)),
             "status_counts": {str(s): int(np.sum(status == s)) for s in np.unique(status)},
+            "acceptance_per_step": acceptance,
             "bin_solves": {str(c): int(np.sum(bins == i)) for i, c in enumerate(BIN_CAPS)},
             "scatter_gather": scat,
             "weak": weak,

@@ -12,10 +12,12 @@ from pathlib import Path
 
 from .build import LIB
 
-ABI_VERSION = 5
-# ABI 4 (round 4) has this cmpc_params layout, bins and solve kernels (its reserved0 was
-# ipm_facts, 0 by default): its builds load only for A/B experiments, with CMPC_ALLOW_ABI4=1
-ABI_COMPAT = (4, 5) if os.environ.get("CMPC_ALLOW_ABI4") == "1" else (5,)
+ABI_VERSION = 6
+# ABI 5 (round 5) has this cmpc_params layout, bins and solve kernels (it lacks cmpc_plan_stats
+# and the certified status-1 bound): its builds load only for A/B experiments, with
+# CMPC_ALLOW_ABI5=1
+ABI_COMPAT = (5, 6) if os.environ.get("CMPC_ALLOW_ABI5") == "1" else (6,)
+NUM_STATS = 4  # CMPC_NUM_STATS
 CMPC_OK = 0
 
 
@@ -48,8 +50,8 @@ EXPORTS = ("cmpc_params_default", "cmpc_plan_create", "cmpc_solve", "cmpc_plan_d
            "cmpc_build_dynamics", "cmpc_solve_warm", "cmpc_solve_ref", "cmpc_generate_traj", "cmpc_leg_torque", "cmpc_srb_step",
            "cmpc_plan_set_timing", "cmpc_plan_timing_read", "cmpc_plan_set_team", "cmpc_plan_team_batch",
            "cmpc_plan_set_heavy_first",
-           "cmpc_plan_heavy_first_batch", "cmpc_plan_solve_kernel", "cmpc_last_error",
-           "cmpc_version")
+           "cmpc_plan_heavy_first_batch", "cmpc_plan_solve_kernel", "cmpc_plan_stats",
+           "cmpc_last_error", "cmpc_version")
 NUM_BINS = 5
 BIN_CAPS = (96, 128, 144, 160, 192)
 # solve kernels (timing slots): 0 = bins NC 128 + 96 (two waves per SIMD), 1 = bins NC 160 + 144,
@@ -118,6 +120,9 @@ def load(path: str | Path | None = None) -> ctypes.CDLL:
         lib.cmpc_plan_set_heavy_first.restype = ctypes.c_int
         lib.cmpc_plan_heavy_first_batch.argtypes = [vp, ctypes.POINTER(ctypes.c_int64)]
         lib.cmpc_plan_heavy_first_batch.restype = ctypes.c_int
+    if hasattr(lib, "cmpc_plan_stats"):
+        lib.cmpc_plan_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+        lib.cmpc_plan_stats.restype = ctypes.c_int
     if hasattr(lib, "cmpc_plan_solve_kernel"):
         lib.cmpc_plan_solve_kernel.argtypes = [vp, ctypes.c_int64, ctypes.c_int]
         lib.cmpc_plan_solve_kernel.restype = ctypes.c_char_p

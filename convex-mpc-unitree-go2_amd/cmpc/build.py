@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import os
 import subprocess
+import sys
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -42,15 +43,25 @@ def build_library(force: bool = False, verbose: bool = False) -> Path:
            f"-I{REPO / 'include'}", f"-I{CSRC}", *map(str, SOURCES), "-o", str(LIB) + ".tmp"]
     if verbose:
         print(" ".join(cmd))
-    try:
-        subprocess.run(cmd, check=True)
-    except subprocess.CalledProcessError:
-        # -amdgpu-mfma-vgpr-form is an internal LLVM option: a compiler that rejects it (or
-        # crashes on a kernel with it) still builds the library, at the spills it avoided
+    r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+    if r.stderr:
+        print(r.stderr, end="", file=sys.stderr)
+    if r.returncode != 0:
+        # -amdgpu-mfma-vgpr-form is an internal LLVM option.  Only a compiler that rejects it or
+        # crashes (not a source error) is retried without it -- and only on explicit request,
+        # since that library spills in the one-wave-per-SIMD kernels (slower, same results)
+        flag_issue = ("amdgpu-mfma-vgpr-form" in r.stderr or r.returncode < 0 or
+                      "PLEASE submit a bug report" in r.stderr)
+        if not (flag_issue and os.environ.get("CMPC_BUILD_ALLOW_NO_VFORM") == "1"):
+            hint = (" (the compiler rejected or crashed on -amdgpu-mfma-vgpr-form: set "
+                    "CMPC_BUILD_ALLOW_NO_VFORM=1 to build without it, at the cost of spills)"
+                    if flag_issue else "")
+            raise RuntimeError(f"cmpc.build: hipcc failed with exit code {r.returncode}{hint}")
         vf = cmd.index("-amdgpu-mfma-vgpr-form")
         cmd = cmd[:vf - 1] + cmd[vf + 1:]
-        print("cmpc.build: WARNING: hipcc failed with -mllvm -amdgpu-mfma-vgpr-form; retrying "
-              "without it (the one-wave-per-SIMD kernels will spill)")
+        print("cmpc.build: WARNING: retrying without -mllvm -amdgpu-mfma-vgpr-form "
+              "(CMPC_BUILD_ALLOW_NO_VFORM=1): the one-wave-per-SIMD kernels will spill",
+              file=sys.stderr)
         subprocess.run(cmd, check=True)
     os.replace(str(LIB) + ".tmp", LIB)
     return LIB

@@ -100,8 +100,8 @@ class Plan:
             if d.abi_version != _lib.ABI_VERSION:
                 if d.abi_version not in _lib.ABI_COMPAT:
                     raise CmpcError(f"cmpc: library ABI {d.abi_version}, this binding is ABI "
-                                    f"{_lib.ABI_VERSION} (an ABI-4 A/B build loads with "
-                                    f"CMPC_ALLOW_ABI4=1)")
+                                    f"{_lib.ABI_VERSION} (an ABI-5 A/B build loads with "
+                                    f"CMPC_ALLOW_ABI5=1)")
                 cp.abi_version = d.abi_version   # (A/B experiments only: same layout and kernels)
             _check(self.lib, self.lib.cmpc_plan_create(ctypes.byref(cp), ctypes.byref(h)),
                    "cmpc_plan_create")
@@ -165,6 +165,17 @@ class Plan:
             r = self.lib.cmpc_plan_solve_kernel(self._h, int(B), k)
             out.append(r.decode() if r else None)
         return out
+
+    def stats(self, reset: bool = False) -> dict:
+        """Acceptance statistics since plan creation or the last reset (cmpc_plan_stats):
+        loose acceptances and the answers returned as status 2 by the certified bound or a
+        stalled downdated refinement.  Synchronises the device."""
+        keys = ("loose", "status2_cert", "status2_stalled", "reserved")
+        if not hasattr(self.lib, "cmpc_plan_stats"):  # (ABI-5 A/B builds)
+            return {k: None for k in keys[:3]}
+        v = (ctypes.c_uint64 * _lib.NUM_STATS)()
+        _check(self.lib, self.lib.cmpc_plan_stats(self._h, v, int(bool(reset))), "cmpc_plan_stats")
+        return {k: int(x) for k, x in zip(keys[:3], list(v))}
 
     def timing_read(self):
         """-> (ms_per_kernel, calls_per_kernel) of the solve kernels since the last read, one

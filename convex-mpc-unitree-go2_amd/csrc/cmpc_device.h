@@ -14,6 +14,7 @@ struct KParams {
   float rho0, sigma, alpha;
   float eps_abs, eps_rel;
   float polish_tol;
+  float r2_min;         // min_i R2[i]: strong-convexity modulus of the condensed objective
   int max_iter;
   int adaptive_interval;
   int polish_stable;
@@ -41,6 +42,10 @@ struct Outputs {
   int32_t* iters;
   float* y;             // nullable: the dual at the returned forces [B][12N]
   float* lam;           // nullable: the reference's multipliers [B][52N] = [lam_x | lam_a]
+  // nullable: per-plan cumulative counters (cmpc_plan_stats): [0] loose acceptances, [1] status 2
+  // because the certified face bound was missed, [2] checks on a stalled downdated refinement
+  // redone on a fresh factorization
+  unsigned long long* stats;
 };
 
 // Free-variable capacities of the LDS bins (3 forces per stance (step, leg)).  Solve kernels

@@ -28,6 +28,7 @@ struct cmpc_plan {
   int device;
   int cus = 0;      // compute units of the device
   int* d_counters;  // counts[kNumBins], heads[kNumBins]
+  unsigned long long* d_stats = nullptr;  // CMPC_NUM_STATS cumulative counters (cmpc_plan_stats)
   int* d_lists;     // kNumBins * max_batch
   float* d_work;    // per-wave park slabs; group k's region starts at work_off[k] (groups overlap)
   size_t work_off[kNumGroups];
@@ -177,9 +178,11 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
   pl->p = *p;
   cmpc::KParams& k = pl->kp;
   k.N = p->N;
+  k.r2_min = 2.f * p->R[0];
   for (int i = 0; i < 12; ++i) {
     k.Q2[i] = 2.f * p->Q[i];
     k.R2[i] = 2.f * p->R[i];
+    k.r2_min = std::min(k.r2_min, k.R2[i]);
   }
   k.mu = p->mu;
   k.fz_min = p->fz_min;
@@ -252,6 +255,11 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
+  if ((e = hipMalloc(&pl->d_stats, CMPC_NUM_STATS * sizeof(unsigned long long))) != hipSuccess ||
+      (e = hipMemset(pl->d_stats, 0, CMPC_NUM_STATS * sizeof(unsigned long long))) != hipSuccess) {
+    cmpc_plan_destroy(pl);
+    return fail(CMPC_E_NOMEM, "hipMalloc stats failed");
+  }
   // the NC 192 stream at the highest priority: its few early waves are dispatched ahead of the
   // register classes submitted right after them on the other queues (solve_impl)
   int prio_lo = 0, prio_hi = 0;
@@ -282,7 +290,7 @@ int cmpc_solve(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const
   if (!Ad || !Bd || !gd || !x0 || !xref || !contact || !w_out || !status || !iters)
     return fail(CMPC_E_INVALID, "cmpc_solve: null array argument");
   return solve_impl(pl, B, cmpc::Inputs{Ad, Bd, gd, x0, xref, contact, nullptr, nullptr, nullptr},
-                    cmpc::Outputs{w_out, status, iters, nullptr, nullptr}, stream);
+                    cmpc::Outputs{w_out, status, iters, nullptr, nullptr, pl->d_stats}, stream);
 }
 
 int cmpc_solve_warm(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd,
@@ -296,7 +304,7 @@ int cmpc_solve_warm(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd,
   if (!Ad || !Bd || !gd || !x0 || !xref || !contact || !w_out || !status || !iters)
     return fail(CMPC_E_INVALID, "cmpc_solve_warm: null array argument");
   return solve_impl(pl, B, cmpc::Inputs{Ad, Bd, gd, x0, xref, contact, w_init, y_init, nullptr},
-                    cmpc::Outputs{w_out, status, iters, y_out, nullptr}, stream);
+                    cmpc::Outputs{w_out, status, iters, y_out, nullptr, pl->d_stats}, stream);
 }
 
 int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, const float* gd,
@@ -310,7 +318,7 @@ int cmpc_solve_ref(cmpc_plan* pl, int64_t B, const float* Ad, const float* Bd, c
   if (!Ad || !Bd || !gd || !x0 || !xref || !contact || !w_out || !status || !iters)
     return fail(CMPC_E_INVALID, "cmpc_solve_ref: null array argument");
   return solve_impl(pl, B, cmpc::Inputs{Ad, Bd, gd, x0, xref, contact, w_init, nullptr, lam_init},
-                    cmpc::Outputs{w_out, status, iters, nullptr, lam_out}, stream);
+                    cmpc::Outputs{w_out, status, iters, nullptr, lam_out, pl->d_stats}, stream);
 }
 
 // group k's persistent kernel with g waves whose park slabs start at wave w0 of the group's
@@ -506,10 +514,7 @@ int cmpc_build_dynamics(cmpc_plan* pl, int64_t B, float dt, const float* mass,
   if (B == 0) return CMPC_OK;
   if (!mass || !inertia || !r_feet || !xref || !Ad || !Bd || !gd)
     return fail(CMPC_E_INVALID, "cmpc_build_dynamics: null array argument");
-#ifndef CMPC_DYN_GRID_CAP
-#define CMPC_DYN_GRID_CAP 8192
-#endif
-  const long long cap = CMPC_DYN_GRID_CAP;
+  const long long cap = 8192;
   const long long blocks = B < cap ? B : cap;  // grid-stride: ~32 resident waves per CU
   hipLaunchKernelGGL(cmpc::dynamics_kernel, dim3((unsigned)blocks), dim3(64), 0,
                      (hipStream_t)stream, pl->kp.N, (double)dt, B, mass, inertia, r_feet, xref, Ad,
@@ -531,10 +536,7 @@ int cmpc_generate_traj(cmpc_plan* pl, int64_t B, double dt, const float* x0, dou
   if (!x0 || !pos_des || !cmd || !t_now || !gait || !foot_lever || !hip || !xref || !contact ||
       !r_feet)
     return fail(CMPC_E_INVALID, "cmpc_generate_traj: null array argument");
-#ifndef CMPC_TRAJ_GRID_CAP
-#define CMPC_TRAJ_GRID_CAP 8192
-#endif
-  const long long cap = CMPC_TRAJ_GRID_CAP;
+  const long long cap = 8192;
   // one wave per group of cmpc::kTrajGroup robots (grid-stride over groups)
   const long long groups = (B + cmpc::kTrajGroup - 1) / cmpc::kTrajGroup;
   const long long blocks = groups < cap ? groups : cap;
@@ -662,7 +664,21 @@ void cmpc_plan_destroy(cmpc_plan* pl) {
   (void)hipFree(pl->d_counters);
   (void)hipFree(pl->d_lists);
   (void)hipFree(pl->d_work);
+  if (pl->d_stats) (void)hipFree(pl->d_stats);
   delete pl;
+}
+
+int cmpc_plan_stats(cmpc_plan* pl, uint64_t* out, int reset) {
+  if (!pl || !out) return fail(CMPC_E_INVALID, "cmpc_plan_stats: null argument");
+  if (int rc = check_device(pl, "cmpc_plan_stats")) return rc;
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  unsigned long long v[CMPC_NUM_STATS];
+  e = hipMemcpy(v, pl->d_stats, sizeof(v), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy stats");
+  for (int i = 0; i < CMPC_NUM_STATS; ++i) out[i] = (uint64_t)v[i];
+  if (reset && (e = hipMemset(pl->d_stats, 0, sizeof(v))) != hipSuccess) return hip_fail(e, "hipMemset stats");
+  return CMPC_OK;
 }
 
 #ifdef CMPC_STAMPS

@@ -47,10 +47,7 @@ struct TrajRobot {
   double off[4];
 };
 
-#ifndef CMPC_TRAJ_GROUP
-#define CMPC_TRAJ_GROUP 16
-#endif
-constexpr int kTrajGroup = CMPC_TRAJ_GROUP;  // robots per wave (enough waves to fill the SIMDs)
+constexpr int kTrajGroup = 16;  // robots per wave (enough waves to fill the SIMDs)
 
 __global__ void __launch_bounds__(64) traj_group_kernel(int N, double dt, int64_t B,
                                                         const float* __restrict__ x0,

@@ -38,35 +38,6 @@
 
 namespace cmpc {
 
-// The one-wave kernels of the bins with NC >= CMPC_LDL_MIN_NC keep a block LDL' factorization
-// of (H + shift I) in the register tiles instead of its inverse (invert_tiles<NC, true>,
-// ldl_apply); 0: none (the explicit inverse of rounds 1-4: -DCMPC_LDL_MIN_NC=0)
-#ifndef CMPC_LDL_MIN_NC
-#define CMPC_LDL_MIN_NC 1
-#endif
-// How ldl_apply turns each block between the row and column layouts:
-//  0: through LDS (write, read back);
-//  1: in registers (DPP / permlane swaps), the D^-1 products formed in the forward sweep -- 2 %
-//     faster on config 3, but its sums run in another order, and with that arithmetic the
-//     next-tick survey drew status-1 answers up to 2e-4 off that the LDS build passes;
-//  2: in registers, with exactly mode 0's arithmetic (bit-identical results: the turned values
-//     are copies; the backward sweep's z rows are read from LDS one block ahead) -- measured
-//     1.3 % slower than mode 0 on config 3 (profiles/r05n_gpu_call.txt);
-//  0 (default): through LDS
-#ifndef CMPC_APPLY_DPP
-#define CMPC_APPLY_DPP 0
-#endif
-constexpr int kApplyMode = CMPC_APPLY_DPP;
-constexpr bool kApplyDpp = kApplyMode == 1;
-template <int NC>
-constexpr bool ldl_for() {
-  return CMPC_LDL_MIN_NC > 0 && NC >= CMPC_LDL_MIN_NC;
-}
-
-#ifndef CMPC_WPE_OVERRIDE
-#define CMPC_WPE_OVERRIDE ((4 * NTL <= 150) ? 2 : 1)
-#endif
-
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -160,36 +131,6 @@ __device__ __forceinline__ float col4_sum(float v) {
 // sum over the wave, result in every lane
 __device__ __forceinline__ float wave_sum(float v) { return col4_sum(row16_sum(v)); }
 
-// Layout turns of a 16-vector without LDS.  Rows layout: every lane of DPP row g holds
-// z[4g .. 4g+3] in its four registers; columns layout: every lane of column c (= lane & 15)
-// holds z[c].
-// rows -> columns: each lane picks z[4g + (c & 3)], then takes the pick of row c >> 2 in its own
-// column (one 16-lane and two 32-lane swaps give every lane its column's four rows)
-__device__ __forceinline__ float rows_to_cols(const f4& zr, int g, int c) {
-  const int q = c & 3;
-  const float t = q == 0 ? zr[0] : q == 1 ? zr[1] : q == 2 ? zr[2] : zr[3];
-  float a0, a1, r0, r2, r1, r3;
-  pair16(t, a0, a1);  // rows (g & 2) and (g & 2) | 1 of this column
-  pair32(a0, r0, r2);
-  pair32(a1, r1, r3);
-  const int src = c >> 2;
-  return src == 0 ? r0 : src == 1 ? r1 : src == 2 ? r2 : r3;
-}
-// columns -> rows: rotate row g right by 16 - 4g (row_ror with a row mask: rows 1, 3 by 12,
-// rows 2, 3 by 8), so lane q of row g holds z[4g + q]; then broadcast lanes 0..3 of each row
-// (row_newbcast)
-template <int CTRL, int ROWS>
-__device__ __forceinline__ float dpp_rows(float old, float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL,
-                                                    ROWS, 0xF, false));
-}
-__device__ __forceinline__ f4 cols_to_rows(float zc) {
-  float t = dpp_rows<0x12C, 0xA>(zc, zc);  // row_ror:12 on rows 1, 3
-  t = dpp_rows<0x128, 0xC>(t, t);          // row_ror:8 on rows 2, 3
-  return f4{dpp_rows<0x150, 0xF>(0.f, t), dpp_rows<0x151, 0xF>(0.f, t),
-            dpp_rows<0x152, 0xF>(0.f, t), dpp_rows<0x153, 0xF>(0.f, t)};
-}
-
 // Lane id the compiler cannot see as loop invariant: every phase re-derives its lane-dependent
 // addresses locally instead of the persistent loops hoisting them (and spilling them) for the
 // whole instance.
@@ -211,6 +152,24 @@ __device__ __forceinline__ int opaque_lane() {
 // attempts, 10 instances, 11 ADMM iterations, 12 gradient calls, 13 symv calls, 29 downdated
 // repairs, 30 downdated faces (16-27: team-mode phases, cmpc_team.hip).
 // ------------------------------------------------------------------------------------------
+// diagnostic build only (-DCMPC_TRACE=id, or -DCMPC_TRACE_IDS=id,id,... to trace several
+// instances inside a full batch): device printf of one instance's ADMM iterations, polish
+// sessions, refinements and KKT checks, every line prefixed with the instance index
+#if defined(CMPC_TRACE_IDS) && !defined(CMPC_TRACE)
+#define CMPC_TRACE (-1)
+#endif
+#ifdef CMPC_TRACE
+__device__ __forceinline__ bool trace_on(int64_t b) {
+#ifdef CMPC_TRACE_IDS
+  constexpr int64_t ids[] = {CMPC_TRACE_IDS};
+  bool on = false;
+  for (int64_t i : ids) on |= (b == i);
+  return on;
+#else
+  return b == CMPC_TRACE;
+#endif
+}
+#endif
 #ifdef CMPC_STAMPS
 __device__ unsigned long long g_stamps[32];
 // (fenced: outstanding memory and LDS traffic completes, no code moves across a stamp; totals
@@ -254,7 +213,7 @@ struct Cfg {
   // per wave (floats): park slab of the register tiles (inverse or LDL' factors)
   static constexpr int SLAB = NTL * 256;
   // registers: the inverse (4 NTL) + working set; two waves per SIMD where it fits in 256
-  static constexpr int WPE = CMPC_WPE_OVERRIDE;
+  static constexpr int WPE = (4 * NTL <= 150) ? 2 : 1;
 };
 
 // Polish sessions and their face sets.  A session starts from ADMM's face set and repairs it
@@ -269,19 +228,6 @@ struct Cfg {
 //  * the starting sets of the last kFailMem failed sessions are remembered; ADMM's face set can
 //    stay "stable" while still wrong, and a session that starts from a remembered set polishes
 //    it once more (it may pass now, from ADMM's better iterate) but makes no repairs.
-// (Knob, off.)  The NC <= 128 bins would start a polish session after polish_stable -
-// CMPC_LIGHT_STABLE_DELTA unchanged ADMM iterations.  With 1, A/B in one gpurun call, two
-// alternations (round 4): config 3 at 65,536 8.65 -> 8.42 ms, config 2 unchanged, config 1 at
-// 256 0.193 -> 0.189 ms, the N = 8 shard rehearsal 1.88 -> 1.81 ms; but it moves which
-// next-tick instance lands on the fp32 KKT check's flat-direction limit, and
-// test_warm_next_tick's warm result 3485 ends 2.11e-4 from the optimum (the test allows 2e-4).
-// Not on until the check can certify those directions.
-#ifndef CMPC_LIGHT_STABLE_DELTA
-#define CMPC_LIGHT_STABLE_DELTA 0
-#endif
-#ifndef CMPC_REFINE_N  // diagnostic override of the refinement count
-#define CMPC_REFINE_N P.polish_refine
-#endif
 constexpr int kRefineExtra = 4;      // polish refinements beyond polish_refine ...
 constexpr float kRefineRate = 0.5f;  // ... while each step shrinks at least this much
 constexpr int kBackoffCap = 3;       // polish back-off doubles per failed session, up to 8x
@@ -298,71 +244,30 @@ constexpr int kLateRepairs = 3;      // repair budget of the sessions after two 
 // config 3 at 8,192 +8 %, config 2 at 65,536 +2 %, config 3 at 65,536 and config 2 at 4,096
 // unchanged; a fixed 2 (without the half) lost 35 % on config 2 at 4,096, a fixed 3 gained
 // nothing on the shards.
-#ifndef CMPC_REPAIR_TOP
-#define CMPC_REPAIR_TOP 2
-#endif
-constexpr int kRepairTop = CMPC_REPAIR_TOP;
+constexpr int kRepairTop = 2;
 // After each failed session (up to kBackoffCap) the face set must stay unchanged 3x longer
 // before the next session: a hard instance's later sessions then start from a settled ADMM
 // iterate instead of re-polishing a set that is still moving (ADMM iterations cost ~1/12 of a
 // factorization).  NumPy model: slowest config-3 instance -21 %.  A/B in one gpurun call (two
 // alternations, with the interior-point fallback off): N = 8 shard rehearsal 2.75 -> 2.43 ms,
 // config 3 at 16,384 3.90 -> 3.65 ms, at 8,192 +3 %, at 65,536 +1 %, config 2 unchanged.
-#ifndef CMPC_STABLE_GROW
-#define CMPC_STABLE_GROW 3
-#endif
-constexpr int kStableGrow = CMPC_STABLE_GROW;
+constexpr int kStableGrow = 3;
 // The NC >= 160 bins also start at rho0 / 2 (round 3; NumPy model: -2.6 % cost in those bins).
 // A/B in one gpurun call, two alternations: config 3 at 65,536 11.43 -> 11.26 ms, config 2 at
 // 65,536 14.05 -> 13.67 ms, at 4,096 2.05 -> 1.95 ms, N = 8 shard rehearsal 2.51 -> 2.38 ms.
-#ifndef CMPC_RHO_LOW_HEAVY
-#define CMPC_RHO_LOW_HEAVY 1
-#endif
-constexpr bool kRhoLowHeavy = CMPC_RHO_LOW_HEAVY;
-#ifndef CMPC_REPAIR_HALF
-#define CMPC_REPAIR_HALF 1
-#endif
-constexpr bool kRepairHalf = CMPC_REPAIR_HALF;
+constexpr bool kRhoLowHeavy = true;
 constexpr int kFailMem = 4;
 constexpr int kTryMem = 8;
-// Face downdates (round 4, face_downdate): a repair that only adds faces downdates the inverse
-// instead of refactoring (team mode: off)
-#ifndef CMPC_DOWNDATE
-#define CMPC_DOWNDATE 1
-#endif
-constexpr bool kDowndate = CMPC_DOWNDATE;
 constexpr float kLooseTol = 5.f;
-// A warm start whose face set fails its polish session restarts as the cold solve (solve_instance)
-#ifndef CMPC_WARM_RESTART
-#define CMPC_WARM_RESTART 1
-#endif
-constexpr bool kWarmRestart = CMPC_WARM_RESTART;
 // Face multipliers in force units (polish_check, nilpotent step with the float64 rollout): a
 // held face's multiplier must be >= -kFaceErr x polish_tol x us x R2 (a force error of at most
-// ~5e-5 relative once released); a loose acceptance allows kLooseFace x that and is status 1
-// only there (a general A's loose acceptance is status 2, not KKT-verified)
-#ifndef CMPC_FACE_ERR
-#define CMPC_FACE_ERR 2.f
-#endif
-constexpr float kFaceErr = CMPC_FACE_ERR;
+// ~5e-5 relative once released); a loose acceptance allows kLooseFace x that
+constexpr float kFaceErr = 2.f;
 constexpr float kLooseFace = 2.5f;
-// polish sessions: give up after CMPC_ABANDON_AFTER repairs whose face set still violates the KKT
-// conditions by more than kAbandonV (relative); 0: never
-#ifndef CMPC_ABANDON_AFTER
-#define CMPC_ABANDON_AFTER 0
-#endif
-constexpr int kAbandonAfter = CMPC_ABANDON_AFTER;
-#ifndef CMPC_ABANDON_V
-#define CMPC_ABANDON_V 1e-2f
-#endif
-constexpr float kAbandonV = CMPC_ABANDON_V;
-// 1: nothing is accepted on a downdated refinement that stalled above the fp32 floor (the face
-// set is refactored first); 0 (default): only a check that ambiguous multipliers alone fail
-// refactors.  Both survey clean on this build; the guard costs 4 % on config 3.
-#ifndef CMPC_STALL_GUARD
-#define CMPC_STALL_GUARD 0
-#endif
-constexpr bool kStallGuard = CMPC_STALL_GUARD;
+// status 1: the held faces' certified force error |c|_2 / min R2 (polish_check's certok) is at
+// most this fraction of the force scale; with the check's primal tolerance (polish_tol, x5 for a
+// loose acceptance, = 5e-5) the returned forces are within ~1e-4 of the optimum
+constexpr float kCertFace = 5e-5f;
 // A check decided by a face multiplier within polish_tol x gs of zero is repeated after up to
 // kAmbRefine more refinement steps (unless the step is already below kAmbConverged x the
 // acceptance tolerance)
@@ -375,10 +280,7 @@ constexpr float kAmbConverged = 1e-2f;
 // a stiffer rho settles ADMM's face set closer to the optimum's before the next session.  NumPy
 // model (tests/algo_spec.py) over 8,192 config-3 / config-2 instances: mean factorizations
 // unchanged, the slowest instance 30 -> 17 (config 3) and 42 -> 26 (config 2) factorizations.
-#ifndef CMPC_FAIL_RHO
-#define CMPC_FAIL_RHO 4.f
-#endif
-constexpr float kFailRho = CMPC_FAIL_RHO;
+constexpr float kFailRho = 4.f;
 
 // Stride of a param's column in Smem::Bt.  (An odd stride, 13, spreads the gradient's per-step
 // column reads over more LDS banks -- 12 puts the 16 steps' columns of a trot on 4 -- but it
@@ -537,21 +439,18 @@ __device__ __forceinline__ void condense_tiles_fwd(Smem<NC>& s, const KParams& P
 
 // ---- software-pipelined sweep (bins up to kSweepPipeMaxNC; measured +3-5 % on NC = 128, and
 // -5 % on cfg2 when also used for the 1-wave-per-SIMD bins, whose registers it spills) ----
-#ifndef CMPC_SWEEP_PIPE_MAX_NC
-#define CMPC_SWEEP_PIPE_MAX_NC 128
-#endif
-constexpr int kSweepPipeMaxNC = CMPC_SWEEP_PIPE_MAX_NC;
+constexpr int kSweepPipeMaxNC = 128;
 // The next 4-pivot step reads only the tiles of its pivot row/column block ("critical" tiles).
 // Each step issues its MFMAs on those tiles first, publishes the next panel from them, and then
 // issues the remaining MFMAs of the step in the same basic block as the next step's LDL and
 // operand build, so that serial chain fills the gaps between MFMAs instead of stalling the wave.
-template <int NC, int K, bool LDL, class SM>
+template <int NC, int K, class SM>
 __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL], int sub,
                                               int g, int c) {
   using C = Cfg<NC>;
   const int c0 = 4 * sub;
   const int pc = c - c0;
-  const bool colw = pc >= 0 && pc < 4, roww = g == sub;
+  const bool colw = pc >= 0 && pc < 4;
   if (colw) {
 #pragma unroll
     for (int I = K; I < C::TT; ++I) {
@@ -564,10 +463,7 @@ __device__ __forceinline__ void sweep_publish(SM& s, const f4 (&M)[Cfg<NC>::NTL]
       for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
     }
   }
-  if (!LDL && roww) {  // (the factorization never reads the swept rows above the block)
-#pragma unroll
-    for (int J = 0; J < K; ++J) *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(K, J)];
-  }
+  // (the factorization never reads the swept rows above the block)
   WSYNC();
 }
 
@@ -615,7 +511,7 @@ __device__ __forceinline__ void sweep_operands(SM& s, int k0, int g, int c,
 }
 
 // rank-4 update of the tiles whose criticality for pivot block Kc is CRIT
-template <int NC, int Kc, bool CRIT, bool LDL, int KMIN>
+template <int NC, int Kc, bool CRIT, int KMIN>
 __device__ __forceinline__ void sweep_mfma(f4 (&M)[Cfg<NC>::NTL], const float (&a)[Cfg<NC>::TT],
                                            const float (&b)[Cfg<NC>::TT], int TA) {
   using C = Cfg<NC>;
@@ -624,7 +520,7 @@ __device__ __forceinline__ void sweep_mfma(f4 (&M)[Cfg<NC>::NTL], const float (&
     if (I >= TA) continue;  // uniform
 #pragma unroll
     for (int J = KMIN; J <= I; ++J) {
-      const bool crit = (J == Kc && I >= Kc) || (!LDL && I == Kc && J < Kc);
+      const bool crit = J == Kc && I >= Kc;
       if (crit != CRIT) continue;  // compile-time after unrolling
       const int t = tile_index(I, J);
       M[t] = mfma4(a[I], b[J], M[t]);
@@ -641,37 +537,37 @@ __device__ __forceinline__ void sweep_diagfix(f4 (&M)[Cfg<NC>::NTL], int sub, in
   for (int q = 0; q < 4; ++q) m[q] -= (roww && pc == q) ? 2.f : 0.f;
 }
 
-template <int NC, int K, bool LDL, class SM>
+template <int NC, int K, class SM>
 __device__ __forceinline__ void sweep_block(SM& s, f4 (&M)[Cfg<NC>::NTL], int ng, int TA,
                                             int g, int c, float (&a)[Cfg<NC>::TT],
                                             float (&b)[Cfg<NC>::TT]) {
   using C = Cfg<NC>;
-  constexpr int KM = LDL ? K : 0;  // first tile column the block's steps update
+  constexpr int KM = K;  // first tile column the block's steps update
   if constexpr (K < C::TT) {
     if (4 * K < ng) {  // uniform
       const int subs = (ng - 4 * K) < 4 ? (ng - 4 * K) : 4;
       for (int sub = 0; sub < subs - 1; ++sub) {  // next step in the same pivot block
-        sweep_mfma<NC, K, true, LDL, KM>(M, a, b, TA);
+        sweep_mfma<NC, K, true, KM>(M, a, b, TA);
         sweep_diagfix<NC, K>(M, sub, g, c);
-        sweep_publish<NC, K, LDL>(s, M, sub + 1, g, c);
-        sweep_mfma<NC, K, false, LDL, KM>(M, a, b, TA);
+        sweep_publish<NC, K>(s, M, sub + 1, g, c);
+        sweep_mfma<NC, K, false, KM>(M, a, b, TA);
         sweep_operands<NC, KM>(s, 16 * K + 4 * (sub + 1), g, c, a, b);
       }
       {  // last step of the block: the next step opens block K + 1
         const int sub = subs - 1;
         const bool has_next = 4 * (K + 1) < ng;
-        sweep_mfma<NC, K + 1, true, LDL, KM>(M, a, b, TA);
+        sweep_mfma<NC, K + 1, true, KM>(M, a, b, TA);
         if constexpr (K + 1 < C::TT) {
-          if (has_next) sweep_publish<NC, K + 1, LDL>(s, M, 0, g, c);
+          if (has_next) sweep_publish<NC, K + 1>(s, M, 0, g, c);
         }
-        sweep_mfma<NC, K + 1, false, LDL, KM>(M, a, b, TA);
+        sweep_mfma<NC, K + 1, false, KM>(M, a, b, TA);
         sweep_diagfix<NC, K>(M, sub, g, c);
         if constexpr (K + 1 < C::TT) {
-          if (has_next) sweep_operands<NC, LDL ? K + 1 : 0>(s, 16 * (K + 1), g, c, a, b);
+          if (has_next) sweep_operands<NC, K + 1>(s, 16 * (K + 1), g, c, a, b);
         }
       }
     }
-    sweep_block<NC, K + 1, LDL>(s, M, ng, TA, g, c, a, b);
+    sweep_block<NC, K + 1>(s, M, ng, TA, g, c, a, b);
   }
 }
 
@@ -981,12 +877,10 @@ template <int NC>
 __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
                                                f4 (&M)[Cfg<NC>::NTL], int n, float shift,
                                                bool nil = false) {
-#ifndef CMPC_NO_NIL
   if (nil) {  // uniform
     condense_tiles_nil<NC>(s, P, M, n, shift);
     return;
   }
-#endif
   if constexpr (NC <= 128) {  // the 1-wave-per-SIMD bins would spill the second form
     if (P.latency_mode) {  // uniform
       condense_tiles_bc<NC>(s, P, M, n, shift);
@@ -997,17 +891,17 @@ __device__ __forceinline__ void condense_tiles(Smem<NC>& s, const KParams& P,
 }
 
 // ------------------------------------------------------------------------------------------
-// block sweep inversion (4 pivots per step, MFMA rank-4 updates)
+// block LDL' factorization by the sweep operator (4 pivots per step, MFMA rank-4 updates)
 // ------------------------------------------------------------------------------------------
-// LDL = true: the same sweep restricted to the tiles right of the swept pivots -- a block LDL'
-// factorization (16-pivot blocks) instead of the inverse, at 4 T(TT - K) MFMAs per block K
-// instead of 4 NTL (T(m) = m (m + 1) / 2: 480 instead of 1,152 for NC = 128).  Sweeping block
-// K on rows / columns >= 16 K leaves -D_K^-1 in tile (K, K) (D_K the Schur-complemented pivot
-// block), L_IK = H_IK D_K^-1 in the tiles below it, and the Schur complement to its right;
-// unscaled, tile (K, K) holds D_K^-1 and tiles (I > J) the unit block-lower L of
-// H = L D L' (applied by ldl_apply).
-template <int NC, bool LDL = false, class SM>
-__device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n) {
+// The symmetric sweep restricted to the tiles right of the swept pivots (round 5; rounds 1-4
+// swept every tile into the explicit inverse): a block LDL' factorization with 16-pivot blocks,
+// 4 T(TT - K) MFMAs per block K instead of 4 NTL (T(m) = m (m + 1) / 2: 480 instead of 1,152 for
+// NC = 128).  Sweeping block K on rows / columns >= 16 K leaves -D_K^-1 in tile (K, K) (D_K the
+// Schur-complemented pivot block), L_IK = H_IK D_K^-1 in the tiles below it, and the Schur
+// complement to its right; unscaled, tile (K, K) holds D_K^-1 and tiles (I > J) the unit
+// block-lower L of H = L D L' (applied by ldl_apply).
+template <int NC, class SM>
+__device__ __forceinline__ void ldl_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n) {
   using C = Cfg<NC>;
   const int lane = opaque_lane();
   const int g = lane >> 4, c = lane & 15;
@@ -1039,9 +933,9 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
   if constexpr (NC <= kSweepPipeMaxNC) {
     if (ng > 0) {
       float a[C::TT], b[C::TT];
-      sweep_publish<NC, 0, LDL>(s, M, 0, g, c);
+      sweep_publish<NC, 0>(s, M, 0, g, c);
       sweep_operands<NC, 0>(s, 0, g, c, a, b);
-      sweep_block<NC, 0, LDL>(s, M, ng, TA, g, c, a, b);
+      sweep_block<NC, 0>(s, M, ng, TA, g, c, a, b);
     }
   } else {
   const bool g1 = g == 1, g2 = g == 2, g3 = g == 3;
@@ -1057,8 +951,8 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
       const int c0 = 4 * sub, k0 = 16 * K + c0;
       const int pc = c - c0;
       const bool colw = pc >= 0 && pc < 4, roww = g == sub;
-      // publish the 4 pivot columns (P^ = P - I on the pivot rows) as panel rows [row][0..3]:
-      // column part from tiles (I >= K, K), row part (transposed) from tiles (K, J < K)
+      // publish the 4 pivot columns (P^ = P - I on the pivot rows) as panel rows [row][0..3]
+      // from tiles (I >= K, K) (the factorization never reads the swept rows above the block)
       if (colw) {
 #pragma unroll
         for (int I = K; I < C::TT; ++I) {
@@ -1070,11 +964,6 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
 #pragma unroll
           for (int q = 0; q < 4; ++q) s.pan[(16 * I + 4 * g + q) * 4 + pc] = m[q];
         }
-      }
-      if (!LDL && roww) {
-#pragma unroll
-        for (int J = 0; J < K; ++J)
-          *reinterpret_cast<f4*>(&s.pan[(16 * J + c) * 4]) = M[tile_index(K, J)];
       }
       WSYNC();
       // D = L diag(dl) L' (unit lower L), so P^ D^-1 P^' = Y diag(1/dl) Y' with Y = P^ L^-T: the
@@ -1106,7 +995,7 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
       const float w2 = g3 ? n32 : g2 ? 1.f : 0.f;
       const float w3 = g3 ? 1.f : 0.f;
       const float ig = g3 ? i3 : g2 ? i2 : g1 ? i1 : i0;
-      const int KM = LDL ? K : 0;  // (a constant once the K loop is unrolled)
+      const int KM = K;  // (a constant once the K loop is unrolled)
       float a[C::TT], b[C::TT];
 #pragma unroll
       for (int I = KM; I < C::TT; ++I) {
@@ -1132,27 +1021,25 @@ __device__ __forceinline__ void invert_tiles(SM& s, f4 (&M)[Cfg<NC>::NTL], int n
     }
   }
   }
-  // M holds -(scaled inverse): undo sign and scaling (LDL: the diagonal tiles hold -(scaled
-  // D_K^-1), the tiles below them the scaled L~ = S^-1 L S)
+  // undo the scaling: the diagonal tiles hold -(scaled D_K^-1), the tiles below them the
+  // scaled L~ = S^-1 L S
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) {
     const f4 ri = *reinterpret_cast<const f4*>(&s.ds[16 * I + 4 * g]);
     f4 rinv;
-    if constexpr (LDL) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) rinv[q] = 1.f / ri[q];
-    }
+    for (int q = 0; q < 4; ++q) rinv[q] = 1.f / ri[q];
 #pragma unroll
     for (int J = 0; J <= I; ++J) {
       const float cj = s.ds[16 * J + c];
       f4& m = M[tile_index(I, J)];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) m[q] *= (LDL && J < I) ? rinv[q] * cj : -(ri[q] * cj);
+      for (int q = 0; q < 4; ++q) m[q] *= (J < I) ? rinv[q] * cj : -(ri[q] * cj);
     }
   }
 }
 
-// out = (L D L')^-1 in over the first n params (factors from invert_tiles<NC, true>; out is
+// out = (L D L')^-1 in over the first n params (factors from ldl_tiles; out is
 // zero beyond n): z = L^-1 in block row by block row (row sums over the block's columns), then
 // x = L'^-1 D^-1 z from the last block row up (column sums over the row's 4-lane groups); each
 // block's result turns layout (rows <-> columns) through `out`, which holds z, then x.
@@ -1167,8 +1054,8 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
   const int TA = (n + 15) >> 4;
   WSYNC();
   float zc[C::TT];  // z by block, column layout (lane c: z[16 J + c])
-  // backward accumulators (column layout, per lane before the 4-group sum): D_I^-1 z_I as the
-  // forward sweep finds z_I (register turns), then minus L_JI' x_J as each x_J is known
+  // backward accumulators (column layout, per lane before the 4-group sum): sum_J L_JI' x_J
+  // as each x_J is known
   float bc[C::TT];
 #pragma unroll
   for (int I = 0; I < C::TT; ++I) bc[I] = 0.f;
@@ -1195,123 +1082,32 @@ __device__ __forceinline__ void ldl_apply(SM& s, const f4 (&M)[Cfg<NC>::NTL], in
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) zr[q] = (16 * I + 4 * g + q < n) ? zr[q] : 0.f;
-    if constexpr (kApplyMode == 1) {
-      zc[I] = rows_to_cols(zr, g, c);
-      const f4 d = M[tile_index(I, I)];
-      bc[I] = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], d[0] * zr[0])));
-    } else if constexpr (kApplyMode == 2) {
-      zc[I] = rows_to_cols(zr, g, c);
-      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
-    } else {
-      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
-      WSYNC();
-      zc[I] = out[16 * I + c];
-    }
+    // the block turns from rows to columns through `out` (a register turn -- DPP / permlane
+    // swaps -- measured 1.3 % slower with this arithmetic, round 5)
+    if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = zr;
+    WSYNC();
+    zc[I] = out[16 * I + c];
   }
   // backward: x_I = D_I^-1 z_I - sum_{J > I} L_JI' x_J
-  f4 zpre = {0.f, 0.f, 0.f, 0.f};  // (mode 2: block I's z rows, read during block I + 1)
-  if constexpr (kApplyMode == 2) WSYNC();
 #pragma unroll
   for (int I = C::TT - 1; I >= 0; --I) {
     if (I >= TA) continue;  // uniform
-    float t;
-    if constexpr (kApplyMode == 1) {
-      t = bc[I];
-    } else if constexpr (kApplyMode == 2) {
-      const f4 zr = (I == TA - 1) ? *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]) : zpre;
-      if (I > 0) zpre = *reinterpret_cast<const f4*>(&out[16 * (I - 1) + 4 * g]);
-      const f4 d = M[tile_index(I, I)];
-      t = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
-    } else {
-      const f4 zr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
-      const f4 d = M[tile_index(I, I)];
-      t = fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
-    }
+    const f4 zr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
+    const f4 d = M[tile_index(I, I)];
+    const float t =
+        fmaf(d[3], zr[3], fmaf(d[2], zr[2], fmaf(d[1], zr[1], fmaf(d[0], zr[0], -bc[I]))));
     float xc = col4_sum(t);
     xc = (16 * I + c < n) ? xc : 0.f;
     WSYNC();
     if (g == 0) out[16 * I + c] = xc;
     if (I == 0) break;
-    f4 xr;
-    if constexpr (kApplyMode != 0) {
-      xr = cols_to_rows(xc);
-    } else {
-      WSYNC();
-      xr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
-    }
+    WSYNC();
+    const f4 xr = *reinterpret_cast<const f4*>(&out[16 * I + 4 * g]);
 #pragma unroll
     for (int J = 0; J < I; ++J) {
       const f4 m = M[tile_index(I, J)];
-      if constexpr (kApplyDpp) {
-        const float u = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], m[0] * xr[0])));
-        bc[J] -= u;
-      } else {
-        bc[J] = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], fmaf(m[0], xr[0], bc[J]))));
-      }
+      bc[J] = fmaf(m[3], xr[3], fmaf(m[2], xr[2], fmaf(m[1], xr[1], fmaf(m[0], xr[0], bc[J]))));
     }
-  }
-  WSYNC();
-  CMPC_ACC(3, t_sv);
-  CMPC_CNT(13, 1);
-}
-
-// out = M in over the first n params (M in register tiles, symmetric, lower triangle stored);
-// `in` is read (and treated as zero) beyond n, out is zero there
-template <int NC, class SM>
-__device__ __forceinline__ void symv(SM& s, const f4 (&M)[Cfg<NC>::NTL], int n,
-                                     const float* in, float* out) {
-  using C = Cfg<NC>;
-  CMPC_T0(t_sv);
-  const int lane = opaque_lane();
-  const int g = lane >> 4, c = lane & 15;
-  n = uniform(n);
-  const int TA = (n + 15) >> 4;
-  WSYNC();
-  float xc[C::TT], cacc[C::TT];
-#pragma unroll
-  for (int J = 0; J < C::TT; ++J) {
-    xc[J] = (16 * J + c < n) ? in[16 * J + c] : 0.f;
-    cacc[J] = 0.f;
-  }
-#pragma unroll
-  for (int I = 0; I < C::TT; ++I) {
-    if (I >= TA) {  // padding rows: zero (uniform branch)
-      if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = f4{0.f, 0.f, 0.f, 0.f};
-      continue;
-    }
-    f4 xr = *reinterpret_cast<const f4*>(&in[16 * I + 4 * g]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xr[q] = (16 * I + 4 * g + q < n) ? xr[q] : 0.f;
-    // packed f32 FMAs (v_pk_fma_f32, the broadcast operand by op_sel): two of the four rows
-    // per instruction
-    f2 r01 = {0.f, 0.f}, r23 = {0.f, 0.f};
-    const f2 x01 = {xr[0], xr[1]}, x23 = {xr[2], xr[3]};
-#pragma unroll
-    for (int J = 0; J <= I; ++J) {
-      const f4 m = M[tile_index(I, J)];
-      const f2 m01 = {m[0], m[1]}, m23 = {m[2], m[3]};
-      const f2 xj = {xc[J], xc[J]};
-      r01 = __builtin_elementwise_fma(m01, xj, r01);
-      r23 = __builtin_elementwise_fma(m23, xj, r23);
-      if (J < I) {
-        f2 cp = m01 * x01;
-        cp = __builtin_elementwise_fma(m23, x23, cp);
-        cacc[J] += cp[0] + cp[1];
-      }
-    }
-    const f4 racc = {r01[0], r01[1], r23[0], r23[1]};
-    // row sums over the 16 lanes of each DPP row -> out rows 16I + 4g + q
-    f4 rs;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) rs[q] = row16_sum(racc[q]);
-    if (c == 0) *reinterpret_cast<f4*>(&out[16 * I + 4 * g]) = rs;
-  }
-  WSYNC();
-#pragma unroll
-  for (int J = 0; J < C::TT; ++J) {
-    if (J >= TA) continue;
-    const float cs = col4_sum(cacc[J]);
-    if (g == 0) out[16 * J + c] += cs;
   }
   WSYNC();
   CMPC_ACC(3, t_sv);
@@ -1459,7 +1255,6 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
       }
     }
   }
-#ifndef CMPC_NO_NIL_GRAD
   if (uniform(s.nil)) {
     // Nilpotent step (A = I + N, N^2 = 0, condense_tiles_nil): A^m = I + m N, so
     //   e_{k+1} = sum_{j<=k} A^{k-j} h_j = S_k + N u_k,   S_k = sum_{j<=k} h_j,
@@ -1552,9 +1347,7 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
 #pragma unroll
       for (int q = 0; q < 3; ++q) s.L[12 * c + 3 * g + q] = Lt[q];
     }
-  } else
-#endif
-  {
+  } else {
   f4 pw[4], tw[4];  // d = 1, 2, 4, 8
   if (pwc != nullptr) {  // (a compile-time constant at every call site)
 #pragma unroll
@@ -1630,12 +1423,11 @@ __device__ __forceinline__ void gradient(Smem<NC>& s, const KParams& P, int n, c
   CMPC_CNT(12, 1);
 }
 
-// M applied to a param vector: the LDL' solve or the register-tile inverse
+// (H + shift)^-1 applied to a param vector: the LDL' solve on the register tiles
 template <int NC, int NT>
 __device__ __forceinline__ void minv_apply(Smem<NC>& s, const KParams& P, const f4 (&M)[NT], int n,
                                            const float* in, float* out) {
-  if constexpr (ldl_for<NC>()) ldl_apply<NC>(s, M, n, in, out);
-  else symv<NC>(s, M, n, in, out);
+  ldl_apply<NC>(s, M, n, in, out);
 }
 
 // Euclidean projection of (a, b, c) onto {|x| <= mu z, |y| <= mu z, z >= fz_min}.
@@ -1816,7 +1608,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
                                              const float* __restrict__ Bg, int ntri, float step,
                                              bool& changed, bool& loose, bool& converged,
                                              bool& amb, bool& decisive, float& vworst,
-                                             int top = 0, bool tr = false) {
+                                             bool& certok, int top = 0, int tr = -1) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
   float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -1872,7 +1664,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
   }
   bool ok = true, am = false, dec = false;
   int nc = 0;
-  float v = 0.f;
+  float v = 0.f, csq = 0.f;
   if (owns) {
     // KKT per triple; on a violation also derive the repaired face set (primal-dual
     // active-set step): drop faces with a negative multiplier, add violated faces
@@ -1897,9 +1689,9 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     v = fmaxf(v, zl ? 0.f : (fzmin - fz) * iu);
     const bool fin = isfinite(fx) && isfinite(fy) && isfinite(fz);
 #ifdef CMPC_TRACE
-    if (tr && (v > 0.f || (sx && lx < tfx) || (sy && ly < tfy) || (zl && l0 < tfz)))
-      printf("      tri %d k %d leg %d code %d f %g %g %g  l %g %g %g  tol %g %g %g  v %g\n", lane, k, leg,
-             code, fx, fy, fz, lx, ly, l0, tfx, tfy, tfz, v);
+    if (tr >= 0 && (v > 0.f || (sx && lx < tfx) || (sy && ly < tfy) || (zl && l0 < tfz)))
+      printf("[%d]       tri %d k %d leg %d code %d f %g %g %g  l %g %g %g  tol %g %g %g  v %g\n", tr,
+             lane, k, leg, code, fx, fy, fz, lx, ly, l0, tfx, tfy, tfz, v);
 #endif
     lok = fin && v <= kLooseTol * P.polish_tol;
     // (precise: a loose acceptance also bounds the force error of every face it holds)
@@ -1909,13 +1701,24 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     s.dl[3 * lane] = fx;  // the candidate, for a loose acceptance by the caller
     s.dl[3 * lane + 1] = fy;
     s.dl[3 * lane + 2] = fz;
+    // certified force error of the held faces (status 1 contract): the point is the exact
+    // optimum of the problem tilted by c = sum_f min(l_f, 0) a_f over the faces it holds
+    // (a = (sx, 0, -mu), (0, sy, -mu), (0, 0, -1)), so |u - u*|_2 <= |c|_2 / min R2 (strong
+    // convexity of the condensed objective, Hessian >= diag(R2))
+    const float nx = sx ? fminf(lx, 0.f) : 0.f, ny = sy ? fminf(ly, 0.f) : 0.f;
+    const float nz = zl ? fminf(l0, 0.f) : 0.f;
+    const float cx = nx * sx, cy = ny * sy, cz = -mu * (nx + ny) - nz;
+    csq = fmaf(cx, cx, fmaf(cy, cy, cz * cz));
+    if (!isfinite(csq)) csq = INFINITY;
   }
+  // (reduced at once, to a uniform bool: nothing of it stays live in vector registers)
+  certok = uniformf(sqrtf(wave_sum(csq))) <= kCertFace * P.r2_min * uniformf(us);
   if (top > 0) {  // uniform: keep the faces of all but the `top` most violated triples
     const bool cand = owns && nc != code;
     float key = cand ? (isfinite(v) ? v : INFINITY) : -1.f;  // a changed triple has v > 0
     bool sel = false;
     const int ncand = __popcll(__ballot(cand));
-    const int kk = kRepairHalf ? max(top, (ncand + 1) >> 1) : top;  // (uniform)
+    const int kk = max(top, (ncand + 1) >> 1);  // (uniform)
     for (int r = 0; r < kk; ++r) {
       const float m = wave_max(key);
       if (!(m > 0.f)) break;  // uniform: no candidate left
@@ -1970,6 +1773,9 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
 // (tests/algo_spec.py downdate=True, the fp32 sweep inverse): unchanged refinement counts, half of
 // all repairs are pure additions, and 6 faces per factorization keep almost all of the gain
 // (config 3: 2.37 -> 2.19 factorizations per instance, the slowest instances -20 %).
+// (diagnostic override only: -DCMPC_DD_CAP=3 exercises the refactor-on-cap path far more often;
+// round 5 recorded its build as run-to-run non-deterministic, round 6's determinism records
+// cover it)
 #ifndef CMPC_DD_CAP
 #define CMPC_DD_CAP 6
 #endif
@@ -2306,8 +2112,11 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 
   int status = -2, iters = 0;
 #ifdef CMPC_DIAG_COUNTS
-  int dg_fact = 0, dg_pol = 0;
+  int dg_fact = 0, dg_pol = 0, dg_flags = 0;
   unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
+  float dg_fail_t[4] = {0.f, 0.f, 0.f, 0.f};  // cycles at the end of failed sessions 1..4
+  int dg_fail_f[4] = {0, 0, 0, 0};            // factorizations by then
+  int dg_nf = 0;
 #endif
 #ifdef CMPC_DIAG_TIMES  // diagnostic build: start / end on the 100 MHz constant clock
   unsigned long long dt_t0 = __builtin_amdgcn_s_memrealtime();
@@ -2354,7 +2163,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         condense_tiles<NC>(s, P, M, nact, uniformf(shift), nil);
         CMPC_ACC(0, t_c);
         CMPC_T0(t_i);
-        invert_tiles<NC, ldl_for<NC>()>(s, M, nact);
+        ldl_tiles<NC>(s, M, nact);
         CMPC_ACC(1, t_i);
       } else {
         CMPC_T0(t_c);
@@ -2371,17 +2180,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       float step = 3.0e38f, prev = 3.0e38f, vscale = 1.f;
       bool ok = false, changed = false, loose = false, converged = false, stalled = false;
       bool decisive = true;
+      bool amb_last = false;  // (trace)
       float vworst = 0.f;
+      bool certok = true;
       for (int pass = 0;; ++pass) {
         // (an extra pass -- ambiguous face multipliers, below -- is one more refinement step)
-        for (int q = pass == 0 ? 0 : CMPC_REFINE_N + kRefineExtra - 1;
-             q < CMPC_REFINE_N + kRefineExtra; ++q) {
+        for (int q = pass == 0 ? 0 : P.polish_refine + kRefineExtra - 1;
+             q < P.polish_refine + kRefineExtra; ++q) {
           gradient<NC, (W > 1), true>(s, P, nact, s.v, s.g, pwc, twc);
           if constexpr (W == 1) {
             minv_apply<NC>(s, P, M, nact, s.g, s.dl);
-            if constexpr (kDowndate) {
-              if (nadd > 0) dd_apply<NC>(s, nact, nadd, s.g, s.dl);  // (uniform)
-            }
+            if (nadd > 0) dd_apply<NC>(s, nact, nadd, s.g, s.dl);  // (uniform)
           } else {
             team_symv_lead<NC, W>(s, *ts, *seq, M, nact, s.g, s.dl);
           }
@@ -2395,10 +2204,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           step = wave_max(m);
           vscale = wave_max(mv);
   #ifdef CMPC_TRACE
-          if (b == CMPC_TRACE && lane == 0) printf("    refine %d step %g\n", q, step);
+          if (trace_on(b) && lane == 0) printf("[%d]     refine %d step %g\n", (int)b, q, step);
   #endif
           stalled = step > kRefineRate * prev;
-          if (q + 1 >= CMPC_REFINE_N && (step <= P.polish_tol * wave_max(mv) || stalled)) break;
+          if (q + 1 >= P.polish_refine && (step <= P.polish_tol * wave_max(mv) || stalled)) break;
           prev = step;
         }
         gradient<NC, (W > 1), true>(s, P, nact, s.v, s.g, pwc, twc);  // E, L at the final point
@@ -2408,11 +2217,12 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         bool amb = false;
   #ifdef CMPC_TRACE
         ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
-                              vworst, top, b == CMPC_TRACE);
+                              vworst, certok, top, trace_on(b) ? (int)b : -1);
   #else
         ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
-                              vworst, top);
+                              vworst, certok, top);
   #endif
+        amb_last = amb;
         // A face multiplier near zero decides the check but moves by ~|H| x the point's remaining
         // error (a step accepted at polish_tol x the force scale leaves ~1e-5 N, i.e. ~1e-7 in a
         // multiplier -- the force-unit tolerance's size: config-3 instance 54289 passed with fz
@@ -2424,9 +2234,11 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           break;
       }
 #ifdef CMPC_TRACE
-      if (b == CMPC_TRACE && lane == 0)
-        printf("it %d polish nact %d nadd %d ok %d loose %d changed %d step %g repairs_left %d\n", it,
-               nact, nadd, (int)ok, (int)loose, (int)changed, step, repairs_left);
+      if (trace_on(b) && lane == 0)
+        printf("[%d] it %d polish nact %d nadd %d ok %d loose %d changed %d amb %d dec %d step %g "
+               "stalled %d repairs_left %d ntried %d nfail %d\n", (int)b, it, nact, nadd, (int)ok,
+               (int)loose, (int)changed, (int)amb_last, (int)decisive, step, (int)stalled,
+               repairs_left, ntried, nfail);
 #endif
       CMPC_ACC(4, t_pol);
       // A refinement on a downdated inverse that stopped contracting above the tight level
@@ -2441,32 +2253,49 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // fp32 floor: the step is then no bound on the point's error (config-3 instance 39503:
       // three downdates, steps 2.2e-4, 5.7e-4, 5.0e-4 against a tolerance of 9.7e-4, accepted
       // 0.037 N = 3.8e-4 off; 25651: one downdate, steps 6.8e-5, 4.3e-5, 1.0e-4, 2.0e-4 off).
-      const bool dd_stall = nadd > 0 && stalled &&
-                            step > kAmbConverged * P.polish_tol * vscale &&
-                            ((kStallGuard && (ok || loose)) || (!ok && !decisive));
-      if (dd_stall) converged = false;
+      // The face set is refactored and refined afresh first (round 6: the guard is the product
+      // rule -- 9.5 % of config-3 instances, 18 % of config 2's, pass a check on such a
+      // refinement, so answering them as status 2 instead was no option; profiles/r06a_*)
+      const bool dd_stalled = nadd > 0 && stalled && step > kAmbConverged * P.polish_tol * vscale;
+      const bool dd_stall = dd_stalled && (ok || loose || !decisive);
+      if (dd_stall) {
+        converged = false;
+        if (out.stats != nullptr && lane == 0) atomicAdd(&out.stats[2], 1ull);  // (rare)
+#ifdef CMPC_DIAG_COUNTS
+        dg_flags |= 4;
+#endif
+      }
+      // status 1 contract (include/cmpc.h): the check passed on a refinement that converged
+      // (and, after downdates, still contracted), and the held faces' certified force error is
+      // within kCertFace of the force scale (nilpotent step: the float64 rollout's
+      // multipliers); a point that misses the bound is returned as status 2
+      const bool cert = !uniform(s.nil) || certok;
       if (ok && !dd_stall) {
+        if (!cert && out.stats != nullptr && lane == 0) atomicAdd(&out.stats[1], 1ull);
+#ifdef CMPC_DIAG_COUNTS
+        if (!cert) dg_flags |= 2;
+#endif
         polished = true;
-        status = 1;
+        status = cert ? 1 : 2;
         break;
       }
       if (nadd > 0 && !converged) {
         // the downdated inverse stopped contracting: refactor the current face set, from the
         // candidate forces (not a repair)
+#ifdef CMPC_TRACE
+        if (trace_on(b) && lane == 0) printf("[%d] it %d STALL-REFACTOR dd_stall %d\n", (int)b, it, (int)dd_stall);
+#endif
         nact = polish_setup<NC>(s, P, Bg, ntri, s.dl);
         nadd = 0;
         shift = P.sigma;
         refactor = true;
         continue;
       }
-      // a session whose face sets are still far off after kAbandonAfter repairs is given up
-      // (back to ADMM) instead of spending its remaining repairs on them
-      const bool hopeless = kAbandonAfter > 0 && ntried > kAbandonAfter && vworst > kAbandonV;
-      if (repairs_left > 0 && changed && !hopeless && !tried_before<NC>(s, ntri, ntried)) {
+      if (repairs_left > 0 && changed && !tried_before<NC>(s, ntri, ntried)) {
         // re-polish on the repaired face set
         --repairs_left;
         bool dd = false;
-        if constexpr (kDowndate && W == 1) {
+        if constexpr (W == 1) {
           // only added faces: downdate the inverse in the current basis (no refactorization)
           const int l = opaque_lane();
           WSYNC();
@@ -2476,6 +2305,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           if (__any((nc & oc) != oc) == 0 && nadd + nf <= dd_max(NC)) {  // (uniform)
             CMPC_T0(t_dd);
             dd = face_downdate<NC>(s, P, M, nact, ntri, nadd);
+#ifdef CMPC_TRACE
+            if (trace_on(b) && lane == 0)
+              printf("[%d] it %d downdate nf %d -> %d nadd %d\n", (int)b, it, nf, (int)dd, nadd);
+#endif
             CMPC_ACC(28, t_dd);
             CMPC_CNT(29, 1);
             CMPC_CNT(30, nf);
@@ -2504,15 +2337,19 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           s.x[3 * l + 2] = pz;
         }
         polished = true;
-        // KKT-verified within the loose bounds only with the float64 rollout (polish_check);
-        // a general A's loose acceptance is reported as not verified
-        status = uniform(s.nil) ? 1 : 2;
+        // KKT-verified within the loose bounds only with the float64 rollout (polish_check) and
+        // the certified face bound; a general A's loose acceptance is reported as not verified
+        status = (uniform(s.nil) && certok) ? 1 : 2;
+        if (out.stats != nullptr && lane == 0) {
+          atomicAdd(&out.stats[0], 1ull);
+          if (!certok) atomicAdd(&out.stats[1], 1ull);
+        }
 #ifdef CMPC_DIAG_COUNTS
-        dg_pol += 100;  // (diagnostic: a loose acceptance)
+        dg_flags |= 1 | (certok ? 0 : 2);
 #endif
         break;
       }
-      if (kWarmRestart && warm_session) {
+      if (warm_session) {
         // The warm face set failed (the state moved across a face change): restart exactly as
         // the cold solve of this problem -- x = z = y = 0, the bin's initial rho, no failed
         // session on record -- so a warm start never takes more ADMM iterations than cold.
@@ -2542,6 +2379,18 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         continue;
       }
       warm_session = false;
+#ifdef CMPC_TRACE
+      if (trace_on(b) && lane == 0)
+        printf("[%d] it %d SESSION-FAIL nfail %d seen %d parked %d rho_low %d fail_rho_done %d nadd %d\n",
+               (int)b, it, nfail, (int)seen_start, (int)parked, (int)rho_low, (int)fail_rho_done, nadd);
+#endif
+#ifdef CMPC_DIAG_COUNTS
+      if (dg_nf < 4) {
+        dg_fail_t[dg_nf] = (float)(__builtin_amdgcn_s_memtime() - dg_t0);
+        dg_fail_f[dg_nf] = dg_fact;
+      }
+      ++dg_nf;
+#endif
       // the session failed: remember its starting face set (unless it came from the memory)
       if (!seen_start) {
         const int l = opaque_lane();
@@ -2643,20 +2492,17 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       }
     }
 #ifdef CMPC_TRACE
-    if (b == CMPC_TRACE) {
+    if (trace_on(b)) {
       const float trp = wave_max(lrp), trd = wave_max(lrd);
-      if (lane == 0) printf("it %d rho %g rp %g rd %g stable %d\n", it, rho, trp, trd, stable);
+      if (lane == 0)
+        printf("[%d] it %d rho %g rp %g rd %g stable %d\n", (int)b, it, rho, trp, trd, stable);
     }
 #endif
     stable = (__any(changed) != 0) ? 0 : stable + 1;
     bool do_pol = false;
     // back off before a further attempt, longer after failed sessions: both the stable run and
     // the distance to the last session grow as polish_stable x 2^min(nfail, kBackoffCap)
-#if CMPC_LIGHT_STABLE_DELTA > 0
-    const int pstable = max(1, P.polish_stable - (NC <= 128 ? CMPC_LIGHT_STABLE_DELTA : 0));
-#else
     const int pstable = P.polish_stable;
-#endif
     const int backoff = pstable << min(nfail, kBackoffCap);
     int need = pstable;  // (kStableGrow: the stable run required grows per failed session)
     for (int f = 0; f < min(nfail, kBackoffCap); ++f) need *= kStableGrow;
@@ -2686,7 +2532,6 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       ++dg_pol;
 #endif
       CMPC_T0(t_ps);
-#ifndef CMPC_NO_PARK
       // Park (write the 36-108 KB inverse to the wave's slab) only where a failed session will
       // restore it: not when a refactor is pending (rho changed: the inverse is stale), not at
       // the NC = 128 bin's reduced rho (a failure refactors at rho0), and not in the first
@@ -2701,12 +2546,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           team_park_store<NC, W, 0>(park, M, 0);
         }
       }
-#else
-      parked = false;      // a failed polish refactors the ADMM matrix instead
-#endif
       repairs_left = session_start<NC>(s, P, ntri, nfail, ntried, seen_start);
       nact = polish_setup<NC>(s, P, Bg, ntri, s.z);
       nadd = 0;
+#ifdef CMPC_TRACE
+      if (trace_on(b) && lane == 0)
+        printf("[%d] it %d SESSION nfail %d parked %d rho %g refactor_pending %d seen %d repairs %d nact %d\n",
+               (int)b, it, nfail, (int)parked, rho, (int)refactor, (int)seen_start, repairs_left, nact);
+#endif
       CMPC_ACC(14, t_ps);
       shift = P.sigma;
       refactor = true;
@@ -2720,6 +2567,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     }
     gradient<NC, (W > 1)>(s, P, n, s.z, s.g, pwc, twc);  // E at u = z (the pure rollout when every leg swings)
   }
+#ifdef CMPC_TRACE
+  if (trace_on(b) && lane == 0) printf("[%d] END status %d iters %d\n", (int)b, status, iters);
+#endif
   CMPC_T0(t_out);
   // ---- outputs: x_{k+1} = e_{k+1} + xref_k, u from the triples (zero on swing legs) ----
   WSYNC();
@@ -2736,6 +2586,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
     wb[NP + o] = uv;
   }
   if (__any(bad)) status = -10;
+#ifdef CMPC_DIAG_COUNTS  // diagnostic build: w[0..7] = cycles and factorizations at failed sessions 1..4
+  if (lane < 4) wb[lane] = dg_fail_t[lane];
+  else if (lane < 8) wb[lane] = (float)dg_fail_f[lane - 4];
+#endif
   if (out.y) {  // dual at the returned forces, in the force layout (zero on swing legs)
     if (polished && n > 0) {  // y = -grad f(u*) (the ADMM fixed point); s.g is the reduced one
       build_admm_basis<NC>(s, P, Bg, ntri);
@@ -2805,7 +2659,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   if (lane == 0) {
 #if defined(CMPC_DIAG_COUNTS)  // diagnostic build: iters | attempts | factorizations, cycles / 16
     out.status[b] = (int)((__builtin_amdgcn_s_memtime() - dg_t0) >> 4);
-    out.iters[b] = iters + 1000 * dg_pol + 1000000 * dg_fact;
+    // (flags: 1 loose acceptance, 2 certified face bound missed, 4 a check on a stalled
+    // downdated refinement redone on a fresh factorization)
+    out.iters[b] = iters + 1000 * (dg_pol + 100 * dg_flags) + 1000000 * dg_fact;
 #elif defined(CMPC_DIAG_TIMES)  // start (10 ns ticks, low 31 bits) | duration + 1e9 if teamed
     out.status[b] = (int)(dt_t0 & 0x7fffffffull);
     out.iters[b] = (int)(__builtin_amdgcn_s_memrealtime() - dt_t0) ;
@@ -2852,10 +2708,7 @@ __device__ __forceinline__ void drain_bin(Smem<NC>& s, const KParams& P, const I
 // exit one by one, the two NC <= 128 waves that take over each freed SIMD then also fit into
 // the LDS it freed: unpadded (27,056 B), the CU's LDS fragmented and the NC <= 128 kernel ran
 // with ~1,550 of its 2,048 waves resident for the rest of the step (tools/shard_anatomy.py).
-#ifndef CMPC_LDS_SLOT
-#define CMPC_LDS_SLOT 19968
-#endif
-constexpr size_t kLdsSlot = CMPC_LDS_SLOT;
+constexpr size_t kLdsSlot = 19968;
 
 // LDS image of a group kernel's bins (NCB = 0: a single-bin kernel)
 template <int NC>

@@ -28,13 +28,21 @@
  *   w_out   [B][24N]           fp32   reference decision layout (centroidal_mpc.py:44,
  *                                      test_MPC.py:190-192): w = [x_1..x_N | u_0..u_{N-1}],
  *                                      each 12 contiguous, i.e. vec(X (12,N),'F') then vec(U,'F')
- *   status  [B]                int32  1 solved (KKT-verified active-set polish: primal
- *                                       feasibility, converged refinement, and every held face's
- *                                       multiplier within a bound that limits the force error
- *                                       its release could cause),
- *                                     2 solved inaccurate (ADMM residuals within eps, or a polish
- *                                       accepted loosely without that bound), -2 max iterations,
- *                                     -10 numerical failure
+ *   status  [B]                int32  1 solved: an active-set polish passed the KKT check --
+ *                                       primal violations <= polish_tol x the force scale us
+ *                                       (<= 5 x for a loose acceptance; the returned forces are
+ *                                       then projected onto the pyramid), a refinement step
+ *                                       <= polish_tol x us that was still contracting (never
+ *                                       one stalled on a face-downdated factorization), and, for
+ *                                       the reference's nilpotent step matrix (float64 rollout),
+ *                                       a CERTIFIED bound on the force error of the held faces:
+ *                                       with c = sum_f min(lambda_f, 0) a_f over the faces held,
+ *                                       |u - u*|_2 <= |c|_2 / min(2R) <= 5e-5 x us (strong
+ *                                       convexity).  Together: within ~1e-4 of the optimum.
+ *                                     2 solved inaccurate: ADMM residuals within eps, or a polished
+ *                                       point that misses the certified bound (returned, but not
+ *                                       verified to 1e-4),
+ *                                     -2 max iterations, -10 numerical failure
  *   iters   [B]                int32  ADMM iterations taken
  *
  * Threading: one plan per host thread / stream.  cmpc_solve is asynchronous on `stream`
@@ -51,10 +59,10 @@
 extern "C" {
 #endif
 
-/* 5: the interior-point variant and its cmpc_plan_set_ipm / cmpc_plan_ipm_batch are gone
- *    (cmpc_params.reserved0 must be 0); status 1 is KKT-verified with face multipliers bounded
- *    in force units.  4: three solve-kernel timing slots. */
-#define CMPC_ABI_VERSION 5
+/* 6: status 1 carries a certified force-error bound (see status above); cmpc_plan_stats.
+ * 5: the interior-point variant and its cmpc_plan_set_ipm / cmpc_plan_ipm_batch are gone
+ *    (cmpc_params.reserved0 must be 0).  4: three solve-kernel timing slots. */
+#define CMPC_ABI_VERSION 6
 
 #define CMPC_OK 0
 #define CMPC_E_INVALID (-22)   /* bad argument / parameter (EINVAL) */
@@ -257,7 +265,12 @@ int cmpc_srb_step(cmpc_plan* plan, int64_t B, int nsub, double dt, const double*
  *                               per kernel, whichever class is submitted first
  *                               (cmpc_plan_set_heavy_first).
  * While enabled, cmpc_solve records a hipEvent pair around each solve-kernel launch on the
- * stream it is launched on; cmpc_plan_timing_read waits for the recorded events, returns the
+ * stream it is launched on -- for slot 2 only the NC 192 kernel's early launch (a few waves on
+ * the highest-priority plan stream, submitted before the classes); its overflow launch, which
+ * drains what those waves left after both classes are done, is not timed.  An event pair spans
+ * the launch's queueing too: with an empty bin the early launch's waves exit at once, but they
+ * are dispatched only when the class kernels free a SIMD, so that span can read milliseconds
+ * while holding nothing.  cmpc_plan_timing_read waits for the recorded events, returns the
  * summed milliseconds per kernel slot (ms_per_kernel[CMPC_NUM_SOLVE_KERNELS]) and the launch
  * counts since the last read, and resets them.  At most 4096 x CMPC_NUM_SOLVE_KERNELS launches
  * are recorded between reads (later ones are not timed). */
@@ -287,6 +300,19 @@ int cmpc_plan_team_batch(const cmpc_plan* plan, int64_t* max_batch);
  * returns the effective bound (0: never). */
 int cmpc_plan_set_heavy_first(cmpc_plan* plan, int64_t min_batch);
 int cmpc_plan_heavy_first_batch(const cmpc_plan* plan, int64_t* min_batch);
+
+/* Acceptance statistics (not on the reference's interface; bench.py reports them): cumulative
+ * counts over every solve with this plan since creation or the last reset, read after a device
+ * synchronisation:
+ *   out[0]  loose acceptances (a polish session that ended on a face set within 5 x polish_tol);
+ *   out[1]  answers returned as status 2 because the certified face bound was missed;
+ *   out[2]  KKT checks that ran on a refinement that had stopped contracting on a face-downdated
+ *           factorization (its step no longer bounds the error): each time the face set was
+ *           refactored and the check redone on a fresh refinement;
+ *   out[3]  reserved (0).
+ * reset != 0 zeroes the counters after reading. */
+#define CMPC_NUM_STATS 4
+int cmpc_plan_stats(cmpc_plan* plan, uint64_t* out, int reset);
 
 /* Thread-local description of the last error returned on this thread ("" if none). */
 const char* cmpc_last_error(void);

@@ -94,6 +94,8 @@ def test_null_arguments(lib):
         assert getattr(lib, name)(None, -1) == -22
         assert name in lib.cmpc_last_error().decode()
     assert lib.cmpc_plan_heavy_first_batch(None, None) == -22
+    assert lib.cmpc_plan_stats(None, None, 0) == -22
+    assert "cmpc_plan_stats" in lib.cmpc_last_error().decode()
     lib.cmpc_plan_destroy(None)
 
 

@@ -131,6 +131,26 @@ def test_deterministic(plan):
     assert np.array_equal(w1, w2) and np.array_equal(s1, s2) and np.array_equal(i1, i2)
 
 
+@pytest.mark.parametrize("cfg", [3, 2])
+def test_instance_order_independent(plan, cfg):
+    """Each instance is one independent solve (centroidal_mpc.py:69-120): its answer must not
+    depend on which instances its wave solved before it.  The batch (16,384 instances: every
+    bin, the one-wave persistent kernels) is solved, then solved again with the instances in a
+    random order, so that each instance lands at another queue position, on another wave, after
+    other instances; the outputs, put back in order, are bitwise equal per instance.  (Round 5's
+    3-downdate-cap build failed this: state read from a previous instance.)"""
+    from cmpc import solve_batch, synth
+    b = synth.make_config(cfg, B=16384)
+    keys = ("Ad", "Bd", "gd", "x0", "xref", "contact")
+    w0, s0, i0 = solve_batch(b, plan=plan)
+    perm = np.random.default_rng(6).permutation(16384)
+    w1, s1, i1 = solve_batch({k: b[k][perm] for k in keys}, plan=plan)
+    inv = np.argsort(perm)
+    w1, s1, i1 = w1[inv], s1[inv], i1[inv]
+    same = np.all(w0.view(np.uint32) == w1.view(np.uint32), axis=1) & (s0 == s1) & (i0 == i1)
+    assert same.all(), (int((~same).sum()), np.flatnonzero(~same)[:8].tolist())
+
+
 def test_class_order_independent():
     """cmpc_plan_set_heavy_first: which register class is submitted first changes only where
     and when each instance runs, never its result (one wave solves it, deterministically).

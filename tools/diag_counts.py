@@ -35,14 +35,21 @@ def main():
         cyc = st.cpu().numpy().astype(np.float64) * 16
         code = it.cpu().numpy().astype(np.int64)
         iters, polraw, fac = code % 1000, (code // 1000) % 1000, code // 1000000
-        loose, pol = polraw // 100, polraw % 100   # (+100 per loose acceptance, cmpc_wave.hip)
+        # (+100 x flags: 1 loose acceptance, 2 certified face bound missed, 4 accepted on a
+        # stalled downdated refinement -- cmpc_wave.hip solve_instance)
+        flags, pol = polraw // 100, polraw % 100
+        loose = flags & 1
         if os.environ.get("CMPC_DIAG_SAVE"):
-            np.savez_compressed(f"{os.environ['CMPC_DIAG_SAVE']}_cfg{cfg}.npz", cyc=cyc, code=code)
+            wh = w[:, :8].cpu().numpy()  # (diag build: cycles / factorizations at failed sessions 1..4)
+            np.savez_compressed(f"{os.environ['CMPC_DIAG_SAVE']}_cfg{cfg}.npz", cyc=cyc, code=code,
+                                fail_t=wh[:, :4], fail_f=wh[:, 4:8])
         order = np.argsort(-cyc)
         tot = cyc.sum()
         print(f"cfg{cfg} {over}: mean cycles {cyc.mean():.0f}  iters mean {iters.mean():.2f}  "
               f"polish {pol.mean():.2f}  fact {fac.mean():.2f}  loose acceptances "
-              f"{int((loose > 0).sum())} of {len(cyc)}")
+              f"{int((loose > 0).sum())} of {len(cyc)}; certified bound missed "
+              f"{int(((flags & 2) > 0).sum())}, stalled downdated refinement "
+              f"{int(((flags & 4) > 0).sum())}")
         for frac in (0.001, 0.01, 0.05):
             k = max(1, int(frac * len(cyc)))
             top = order[:k]
