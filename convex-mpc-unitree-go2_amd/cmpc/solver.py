@@ -170,7 +170,7 @@ class Plan:
         """Acceptance statistics since plan creation or the last reset (cmpc_plan_stats):
         loose acceptances and the answers returned as status 2 by the certified bound or a
         stalled downdated refinement.  Synchronises the device."""
-        keys = ("loose", "status2_cert", "status2_stalled", "reserved")
+        keys = ("loose", "status2_cert", "guard_refactors", "reserved")
         if not hasattr(self.lib, "cmpc_plan_stats"):  # (ABI-5 A/B builds)
             return {k: None for k in keys[:3]}
         v = (ctypes.c_uint64 * _lib.NUM_STATS)()

@@ -264,7 +264,7 @@ constexpr float kLooseTol = 5.f;
 // ~5e-5 relative once released); a loose acceptance allows kLooseFace x that
 constexpr float kFaceErr = 2.f;
 constexpr float kLooseFace = 2.5f;
-// status 1: the held faces' certified force error |c|_2 / min R2 (polish_check's certok) is at
+// status 1: the held faces' certified force error |c|_2 / min R2 (certified_faces) is at
 // most this fraction of the force scale; with the check's primal tolerance (polish_tol, x5 for a
 // loose acceptance, = 5e-5) the returned forces are within ~1e-4 of the optimum
 constexpr float kCertFace = 5e-5f;
@@ -1608,7 +1608,7 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
                                              const float* __restrict__ Bg, int ntri, float step,
                                              bool& changed, bool& loose, bool& converged,
                                              bool& amb, bool& decisive, float& vworst,
-                                             bool& certok, int top = 0, int tr = -1) {
+                                             int top = 0, int tr = -1) {
   const int lane = opaque_lane();
   const float mu = P.mu, fzmin = P.fz_min;
   float fx = 0.f, fy = 0.f, fz = 0.f;
@@ -1711,8 +1711,10 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
     csq = fmaf(cx, cx, fmaf(cy, cy, cz * cz));
     if (!isfinite(csq)) csq = INFINITY;
   }
-  // (reduced at once, to a uniform bool: nothing of it stays live in vector registers)
-  certok = uniformf(sqrtf(wave_sum(csq))) <= kCertFace * P.r2_min * uniformf(us);
+  // (parked in the ADMM scratch s.r, which nothing reads before the next ADMM iteration or
+  // face downdate rewrites it: certified_faces reduces it only for an accepted point)
+  s.r[lane] = owns ? csq : 0.f;
+  if (lane == 0) s.r[64] = us;
   if (top > 0) {  // uniform: keep the faces of all but the `top` most violated triples
     const bool cand = owns && nc != code;
     float key = cand ? (isfinite(v) ? v : INFINITY) : -1.f;  // a changed triple has v > 0
@@ -1754,6 +1756,16 @@ __device__ __forceinline__ bool polish_check(Smem<NC>& s, const KParams& P,
 }
 
 // ------------------------------------------------------------------------------------------
+// The certified force error of the held faces at the point polish_check accepted (its per-triple
+// |c_t|^2 and the force scale are in s.r): within kCertFace of the force scale?  Uniform.
+template <int NC>
+__device__ __forceinline__ bool certified_faces(Smem<NC>& s, const KParams& P) {
+  const int lane = opaque_lane();
+  WSYNC();
+  const float c2 = wave_sum(s.r[lane]);
+  return uniformf(sqrtf(c2)) <= kCertFace * P.r2_min * uniformf(s.r[64]);
+}
+
 // Face downdates (round 4).  A repair that only ADDS faces to the current face set keeps the
 // basis and the inverse M of the last factorization: each added face is an equality a'v = c on
 // the basis params (fz at fz_min: v_pz = fz_min; fx on the face of sign s: v_px - s mu v_pz = 0,
@@ -2131,6 +2143,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   int it = 0;
   int repairs_left = 0;
   int nadd = 0;           // faces added by downdates since the last factorization
+  bool from_cand = false; // the polish refactored from a candidate that passed its check
   bool parked = false;    // the ADMM inverse is in the park slab
   int nfail = 0;          // failed sessions so far (the memory holds the last kFailMem)
   int ntried = 0;         // face sets tried in the current session
@@ -2182,7 +2195,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       bool decisive = true;
       bool amb_last = false;  // (trace)
       float vworst = 0.f;
-      bool certok = true;
+      // refinement steps before the convergence test may stop them: polish_refine from ADMM's
+      // rough point; one from a candidate that already passed the check (a stall re-check)
+      const int qmin = from_cand ? 1 : P.polish_refine;
+      from_cand = false;
       for (int pass = 0;; ++pass) {
         // (an extra pass -- ambiguous face multipliers, below -- is one more refinement step)
         for (int q = pass == 0 ? 0 : P.polish_refine + kRefineExtra - 1;
@@ -2207,7 +2223,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           if (trace_on(b) && lane == 0) printf("[%d]     refine %d step %g\n", (int)b, q, step);
   #endif
           stalled = step > kRefineRate * prev;
-          if (q + 1 >= P.polish_refine && (step <= P.polish_tol * wave_max(mv) || stalled)) break;
+          if (q + 1 >= qmin && (step <= P.polish_tol * wave_max(mv) || stalled)) break;
           prev = step;
         }
         gradient<NC, (W > 1), true>(s, P, nact, s.v, s.g, pwc, twc);  // E, L at the final point
@@ -2217,10 +2233,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         bool amb = false;
   #ifdef CMPC_TRACE
         ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
-                              vworst, certok, top, trace_on(b) ? (int)b : -1);
+                              vworst, top, trace_on(b) ? (int)b : -1);
   #else
         ok = polish_check<NC>(s, P, Bg, ntri, step, changed, loose, converged, amb, decisive,
-                              vworst, certok, top);
+                              vworst, top);
   #endif
         amb_last = amb;
         // A face multiplier near zero decides the check but moves by ~|H| x the point's remaining
@@ -2269,8 +2285,8 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // (and, after downdates, still contracted), and the held faces' certified force error is
       // within kCertFace of the force scale (nilpotent step: the float64 rollout's
       // multipliers); a point that misses the bound is returned as status 2
-      const bool cert = !uniform(s.nil) || certok;
       if (ok && !dd_stall) {
+        const bool cert = !uniform(s.nil) || certified_faces<NC>(s, P);
         if (!cert && out.stats != nullptr && lane == 0) atomicAdd(&out.stats[1], 1ull);
 #ifdef CMPC_DIAG_COUNTS
         if (!cert) dg_flags |= 2;
@@ -2289,6 +2305,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         nadd = 0;
         shift = P.sigma;
         refactor = true;
+        from_cand = ok || loose;  // (the guard: the candidate passed; its error is what is checked)
         continue;
       }
       if (repairs_left > 0 && changed && !tried_before<NC>(s, ntri, ntried)) {
@@ -2327,6 +2344,7 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         continue;
       }
       if (loose) {  // the session ends on a set within the loose tolerance: accept it
+        const bool certok = certified_faces<NC>(s, P);
         const int l = opaque_lane();
         WSYNC();
         if (l < ntri) {  // (projected onto the pyramid: the loose check admits 5x polish_tol)

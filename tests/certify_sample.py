@@ -54,11 +54,15 @@ def batch_of(name):
     raise KeyError(name)
 
 
-def gpu(sets):
+def gpu(sets, lib=None, params=()):
     import torch
+    from cmpc import _lib
+    if lib:  # a variant build (A/B surveys)
+        _lib._lib = _lib.load(lib)
     from cmpc import Plan, SolverParams, to_device_batch
     DIR.mkdir(parents=True, exist_ok=True)
-    plan = Plan(SolverParams(max_batch=65536))
+    over = {k: type(getattr(SolverParams, k))(float(v)) for k, v in (a.split("=") for a in params)}
+    plan = Plan(SolverParams(max_batch=65536, **over))
     for name in sets:
         t0 = time.time()
         b, prev = batch_of(name)
@@ -167,6 +171,8 @@ if __name__ == "__main__":
     ap.add_argument("--sets", default=",".join(ALL))
     ap.add_argument("--procs", type=int, default=16)
     ap.add_argument("--report", default=str(REPO / "gpurun_out" / "parity_survey.txt"))
+    ap.add_argument("--lib", default=None, help="gpu phase: a variant library")
+    ap.add_argument("--param", action="append", default=[], help="gpu phase: SolverParams name=value")
     a = ap.parse_args()
     sets = [s for s in a.sets.split(",") if s]
-    gpu(sets) if a.mode == "gpu" else cpu(sets, a.procs, a.report)
+    gpu(sets, a.lib, a.param) if a.mode == "gpu" else cpu(sets, a.procs, a.report)

@@ -53,6 +53,17 @@ def feasibility(batch, U, mu=0.8, fz_min=10.0):
     return np.maximum(v_sw, v_st).reshape(U.shape[0], -1).max(1)
 
 
+def assert_verified(st, max_unverified=1e-4):
+    """A large synthetic batch: every instance solved, status 1 (KKT-verified, within 1e-4 of the
+    optimum by the certified bound, include/cmpc.h) except at most a max_unverified fraction at
+    status 2 -- a polished point that missed the certified face bound and is returned without
+    the 1e-4 guarantee (config 3: 1 of 65,536).  Returns the status-1 mask."""
+    st = np.asarray(st)
+    assert np.all((st == 1) | (st == 2)), np.unique(st, return_counts=True)
+    assert np.sum(st == 2) <= max(1, int(max_unverified * len(st))), np.flatnonzero(st == 2)[:16]
+    return st == 1
+
+
 def input_digest(batch, idx):
     """sha256 of the fp32 boundary inputs of instances `idx` (detects generator drift between
     the fixture's generation and the test)."""
