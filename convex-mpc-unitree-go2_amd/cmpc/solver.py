@@ -36,7 +36,7 @@ class SolverParams:
     alpha: float = 1.6
     adaptive_rho_interval: int = 25
     polish_stable: int = 3
-    polish_refine: int = 4
+    polish_refine: int = 2
     polish_tol: float = 1e-5
     polish_repairs: int = 6
     check_termination: int = 1   # OPTS check_termination (reference: 10; include/cmpc.h)

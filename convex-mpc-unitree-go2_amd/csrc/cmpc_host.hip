@@ -140,7 +140,7 @@ void cmpc_params_default(cmpc_params* p) {
   p->alpha = 1.6f;     // OSQP default
   p->adaptive_rho_interval = 25;  // centroidal_mpc.py:32
   p->polish_stable = 3;
-  p->polish_refine = 4;
+  p->polish_refine = 2;  // (round 6: 4 -> 2 with the LDL' solve; profiles/r06d_*)
   p->polish_tol = 1e-5f;
   p->polish_repairs = 6;
   p->reserved0 = 0;

@@ -88,7 +88,8 @@ typedef struct cmpc_params {
   float alpha;            /* over-relaxation (OSQP alpha) */
   int32_t adaptive_rho_interval; /* iterations between rho updates (0 = off) */
   int32_t polish_stable;  /* polish after the active set is unchanged this many iterations */
-  int32_t polish_refine;  /* iterative-refinement steps inside the polish */
+  int32_t polish_refine;  /* refinement steps inside the polish before its convergence test may
+                             stop them (up to 4 more while the step still halves); default 2 */
   float polish_tol;       /* relative KKT tolerance for accepting the polished point */
   int32_t polish_repairs; /* active-set repairs (add violated / drop negative-multiplier faces
                              and re-polish) before resuming ADMM */
