@@ -255,8 +255,7 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
     delete pl;
     return fail(CMPC_E_NOMEM, "hipMalloc lists failed");
   }
-  if ((e = hipMalloc(&pl->d_stats, CMPC_NUM_STATS * sizeof(unsigned long long))) != hipSuccess ||
-      (e = hipMemset(pl->d_stats, 0, CMPC_NUM_STATS * sizeof(unsigned long long))) != hipSuccess) {
+  if ((e = hipMalloc(&pl->d_stats, CMPC_NUM_STATS * sizeof(unsigned long long))) != hipSuccess) {
     cmpc_plan_destroy(pl);
     return fail(CMPC_E_NOMEM, "hipMalloc stats failed");
   }
@@ -271,6 +270,15 @@ int cmpc_plan_create(const cmpc_params* p, cmpc_plan** out) {
       (e = hipEventCreateWithFlags(&pl->join_top, hipEventDisableTiming)) != hipSuccess) {
     cmpc_plan_destroy(pl);
     return hip_fail(e, "side stream/event creation");
+  }
+  // zeroed on the plan's own stream: a copy or memset on the null stream here (the caller's
+  // default stream, round 6's first ABI-6 build) made the closed loop's HIP-graph replay at
+  // 65,536 robots 1.3x slower than eager (profiles/r06l_*)
+  if ((e = hipMemsetAsync(pl->d_stats, 0, CMPC_NUM_STATS * sizeof(unsigned long long), pl->side)) !=
+          hipSuccess ||
+      (e = hipStreamSynchronize(pl->side)) != hipSuccess) {
+    cmpc_plan_destroy(pl);
+    return hip_fail(e, "hipMemsetAsync stats");
   }
   *out = pl;
   g_err.clear();
@@ -673,11 +681,13 @@ int cmpc_plan_stats(cmpc_plan* pl, uint64_t* out, int reset) {
   if (int rc = check_device(pl, "cmpc_plan_stats")) return rc;
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  // (on the plan's stream, not the null stream: see cmpc_plan_create)
   unsigned long long v[CMPC_NUM_STATS];
-  e = hipMemcpy(v, pl->d_stats, sizeof(v), hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "hipMemcpy stats");
+  if ((e = hipMemcpyAsync(v, pl->d_stats, sizeof(v), hipMemcpyDeviceToHost, pl->side)) != hipSuccess ||
+      (reset && (e = hipMemsetAsync(pl->d_stats, 0, sizeof(v), pl->side)) != hipSuccess) ||
+      (e = hipStreamSynchronize(pl->side)) != hipSuccess)
+    return hip_fail(e, "cmpc_plan_stats copy");
   for (int i = 0; i < CMPC_NUM_STATS; ++i) out[i] = (uint64_t)v[i];
-  if (reset && (e = hipMemset(pl->d_stats, 0, sizeof(v))) != hipSuccess) return hip_fail(e, "hipMemset stats");
   return CMPC_OK;
 }
 

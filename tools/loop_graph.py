@@ -1,6 +1,6 @@
 """Diagnostic: the closed-loop tick (cmpc/closed_loop.py) eager vs HIP-graph replay on the same
 tick sequence -- per-tick wall time of each mode, for rocprofv3 kernel traces of both.
-   usage: python tools/loop_graph.py [B] [ticks]"""
+   usage: python tools/loop_graph.py [B] [ticks] [lib] [modes: eager,graph,eager2,graph2,graphsync]"""
 import functools
 import sys
 import time
@@ -15,6 +15,9 @@ sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 
 def main():
     import torch
+    from cmpc import _lib
+    if len(sys.argv) > 3:
+        _lib._lib = _lib.load(sys.argv[3])
     from cmpc import Plan, SolverParams
     from cmpc.closed_loop import ClosedLoop
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
@@ -24,7 +27,8 @@ def main():
     cmd = np.stack([rg.uniform(-0.5, 0.5, B), rg.uniform(-0.2, 0.2, B), np.full(B, 0.27),
                     rg.uniform(-1, 1, B)], 1)
     res = {}
-    for mode in ("eager", "graph", "eager2", "graph2"):
+    modes = sys.argv[4].split(",") if len(sys.argv) > 4 else ["eager", "graph", "eager2", "graph2"]
+    for mode in modes:
         cl = ClosedLoop(B, plan=plan, seed=0)
         cl.set_command(cmd)
         for _ in range(4):
@@ -36,6 +40,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(T):
             cl.tick()
+            if mode.endswith("sync"):  # no replay queued behind the running one
+                torch.cuda.synchronize()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         res[mode] = el / T * 1e3
