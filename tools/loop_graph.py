@@ -16,7 +16,7 @@ sys.path.insert(0, str(REPO / "convex-mpc-unitree-go2_amd"))
 def main():
     import torch
     from cmpc import _lib
-    if len(sys.argv) > 3:
+    if len(sys.argv) > 3 and sys.argv[3]:
         _lib._lib = _lib.load(sys.argv[3])
     from cmpc import Plan, SolverParams
     from cmpc.closed_loop import ClosedLoop
