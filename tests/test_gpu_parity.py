@@ -170,6 +170,23 @@ def test_class_order_independent():
     assert np.array_equal(w0, w1) and np.array_equal(s0, s1) and np.array_equal(i0, i1)
 
 
+def test_plan_stats(plan):
+    """cmpc_plan_stats (ABI 6, include/cmpc.h): the acceptance counters start at zero after a
+    reset, count the same events when the same batch is solved again (the solver is
+    deterministic), and a certified-bound miss is always an answer returned as status 2."""
+    from cmpc import solve_batch, synth
+    b = synth.make_config(3, B=16384)
+    plan.stats(reset=True)
+    assert plan.stats() == {"loose": 0, "status2_cert": 0, "guard_refactors": 0}
+    _, s0, _ = solve_batch(b, plan=plan)
+    a = plan.stats(reset=True)
+    _, s1, _ = solve_batch(b, plan=plan)
+    assert plan.stats(reset=True) == a
+    assert np.array_equal(s0, s1)
+    assert min(a.values()) >= 0 and a["loose"] + a["guard_refactors"] > 0, a
+    assert a["status2_cert"] <= int((s0 == 2).sum()), (a, int((s0 == 2).sum()))
+
+
 def test_full_size_certified_sample(plan):
     """The full config-3 batch (65,536 trot + mixed, the headline workload) in one solve: every
     instance solved and feasible -- status 1 but for at most a 1e-4 fraction at status 2 (a
