@@ -311,7 +311,9 @@ int cmpc_plan_heavy_first_batch(const cmpc_plan* plan, int64_t* min_batch);
  *           factorization (its step no longer bounds the error): each time the face set was
  *           refactored and the check redone on a fresh refinement;
  *   out[3]  reserved (0).
- * reset != 0 zeroes the counters after reading. */
+ * reset != 0 zeroes the counters after reading.  The copy and the reset run on the plan's own
+ * stream, never on the null stream (a null-stream operation from the library slowed the
+ * caller's later HIP-graph replays). */
 #define CMPC_NUM_STATS 4
 int cmpc_plan_stats(cmpc_plan* plan, uint64_t* out, int reset);
 
