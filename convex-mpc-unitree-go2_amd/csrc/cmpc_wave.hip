@@ -2168,6 +2168,10 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   while (n > 0) {
     if (refactor) {  // the only condense + invert call site
       CMPC_CNT(8, 1);
+#ifdef CMPC_TRACE
+      if (trace_on(b) && lane == 0)
+        printf("[%d] it %d FACTOR polish %d nact %d shift %g\n", (int)b, it, (int)in_polish, nact, shift);
+#endif
 #ifdef CMPC_DIAG_COUNTS
       ++dg_fact;
 #endif
@@ -2319,6 +2323,14 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
           const int oc = (l < ntri) ? s.code[l] : 0, nc = (l < ntri) ? s.tcnt[l] : 0;
           const int add = nc & ~oc;
           const int nf = wave_total4((add & 1) + ((add & 6) != 0) + ((add & 24) != 0));
+#ifdef CMPC_TRACE
+          {
+            const bool drop = __any((nc & oc) != oc), freed = __any(((nc ^ oc) & oc & 1) != 0);
+            if (trace_on(b) && lane == 0)
+              printf("[%d] it %d repair drop %d (fz face freed %d) nf %d nadd %d cap %d\n", (int)b,
+                     it, (int)drop, (int)freed, nf, nadd, dd_max(NC));
+          }
+#endif
           if (__any((nc & oc) != oc) == 0 && nadd + nf <= dd_max(NC)) {  // (uniform)
             CMPC_T0(t_dd);
             dd = face_downdate<NC>(s, P, M, nact, ntri, nadd);
