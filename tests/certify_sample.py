@@ -18,6 +18,7 @@ GPU.  Sets (the parity bar is 1e-4 on every status-1 instance):
   cfg3_65536       the headline batch (config 3, 65,536), cold, every instance
   cfg3_next_warm   the headline batch's next tick warm-started from its (w, y_out), every instance
   cfg2_65536       config 2's distribution at 65,536, cold, every instance
+  (--sets with EXTRA: mixed_s11_65536, trot_s12_65536 cold and mixed_s13_next_warm, fresh seeds)
 """
 import argparse
 import json
@@ -34,6 +35,8 @@ sys.path[:0] = [str(REPO / "tests"), str(REPO), str(REPO / "convex-mpc-unitree-g
 DIR = Path(os.environ.get("SURVEY_DIR", "/tmp/cmpc_survey"))
 ALL = ("cfg2_next_cold", "cfg2_next_warm", "cfg2_next_ref", "cfg2_4096", "cfg1_256",
        "cfg3_65536", "cfg3_next_warm", "cfg2_65536")
+# fresh seeds (round 6): problems no test, fixture or tuning run has seen
+EXTRA = ("mixed_s11_65536", "trot_s12_65536", "mixed_s13_next_warm")
 
 
 def batch_of(name):
@@ -51,6 +54,13 @@ def batch_of(name):
         return synth.next_tick(synth.make_config(3)), synth.make_config(3)
     if name == "cfg2_65536":
         return synth.make_config(2, B=65536), None
+    if name == "mixed_s11_65536":
+        return synth.make_batch(65536, 11, mixed=True), None
+    if name == "trot_s12_65536":
+        return synth.make_batch(65536, 12, mixed=False), None
+    if name == "mixed_s13_next_warm":
+        b = synth.make_batch(65536, 13, mixed=True)
+        return synth.next_tick(b), b
     raise KeyError(name)
 
 
