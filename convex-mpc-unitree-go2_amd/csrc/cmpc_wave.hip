@@ -1766,6 +1766,24 @@ __device__ __forceinline__ bool certified_faces(Smem<NC>& s, const KParams& P) {
   return uniformf(sqrtf(c2)) <= kCertFace * P.r2_min * uniformf(s.r[64]);
 }
 
+#ifdef CMPC_DIAG_GRES
+// diagnostic build: at an accepted point, |grad|_2 (the gradient at the final refinement point,
+// s.g over the nact params) and |c|_2, both over min 2R x the force scale (force-error units)
+template <int NC>
+__device__ __forceinline__ void diag_gres(Smem<NC>& s, const KParams& P, int nact, float& gm,
+                                          float& cm, float& us) {
+  const int lane = opaque_lane();
+  WSYNC();
+  float g2 = 0.f;
+  for (int p = lane; p < nact; p += 64) g2 = fmaf(s.g[p], s.g[p], g2);
+  g2 = wave_sum(g2);
+  const float c2 = wave_sum(s.r[lane]);
+  us = uniformf(s.r[64]);
+  gm = uniformf(sqrtf(g2)) / (P.r2_min * us);
+  cm = uniformf(sqrtf(c2)) / (P.r2_min * us);
+}
+#endif
+
 // Face downdates (round 4).  A repair that only ADDS faces to the current face set keeps the
 // basis and the inverse M of the last factorization: each added face is an equality a'v = c on
 // the basis params (fz at fz_min: v_pz = fz_min; fx on the face of sign s: v_px - s mu v_pz = 0,
@@ -2123,6 +2141,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
   // ADMM state (x, z, y of triple t at 3t .. 3t+2) lives in LDS, not in registers
 
   int status = -2, iters = 0;
+#ifdef CMPC_DIAG_GRES
+  float dg_gm = -1.f, dg_cm = -1.f, dg_us = 0.f;  // (-1: not a polished point)
+#endif
 #ifdef CMPC_DIAG_COUNTS
   int dg_fact = 0, dg_pol = 0, dg_flags = 0;
   unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
@@ -2290,6 +2311,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
       // within kCertFace of the force scale (nilpotent step: the float64 rollout's
       // multipliers); a point that misses the bound is returned as status 2
       if (ok && !dd_stall) {
+#ifdef CMPC_DIAG_GRES
+        diag_gres<NC>(s, P, nact, dg_gm, dg_cm, dg_us);
+#endif
         const bool cert = !uniform(s.nil) || certified_faces<NC>(s, P);
         if (!cert && out.stats != nullptr && lane == 0) atomicAdd(&out.stats[1], 1ull);
 #ifdef CMPC_DIAG_COUNTS
@@ -2356,6 +2380,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
         continue;
       }
       if (loose) {  // the session ends on a set within the loose tolerance: accept it
+#ifdef CMPC_DIAG_GRES
+        diag_gres<NC>(s, P, nact, dg_gm, dg_cm, dg_us);
+#endif
         const bool certok = certified_faces<NC>(s, P);
         const int l = opaque_lane();
         WSYNC();
@@ -2619,6 +2646,9 @@ __device__ __forceinline__ void solve_instance(Smem<NC>& s, const KParams& P, in
 #ifdef CMPC_DIAG_COUNTS  // diagnostic build: w[0..7] = cycles and factorizations at failed sessions 1..4
   if (lane < 4) wb[lane] = dg_fail_t[lane];
   else if (lane < 8) wb[lane] = (float)dg_fail_f[lane - 4];
+#endif
+#ifdef CMPC_DIAG_GRES  // diagnostic build: w[0..2] = the gradient and face metrics, the force scale
+  if (lane == 0) { wb[0] = dg_gm; wb[1] = dg_cm; wb[2] = dg_us; }
 #endif
   if (out.y) {  // dual at the returned forces, in the force layout (zero on swing legs)
     if (polished && n > 0) {  // y = -grad f(u*) (the ADMM fixed point); s.g is the reduced one

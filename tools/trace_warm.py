@@ -2,7 +2,7 @@
 iterations, polish sessions, refinements, repairs and the final status of those indices).
 The previous tick is solved cold first (its trace lines come before the "== warm" marker), then
 the next tick (synth.next_tick) warm from its (w, y_out).
-   usage: python tools/trace_warm.py LIB SEED [mixed=1]   (GPU)"""
+   usage: python tools/trace_warm.py LIB SEED [mixed=1] [ID,ID,...: save their rows]   (GPU)"""
 import functools
 import sys
 from pathlib import Path
@@ -32,9 +32,11 @@ def main():
     w, st, it, _ = plan.solve(d["Ad"], d["Bd"], d["gd"], d["x0"], d["xref"], d["contact"],
                               w_init=w0, y_init=y0, y_out=True)
     torch.cuda.synchronize()
-    np.savez(REPO / "gpurun_out" / "trace_warm.npz", w=w.cpu().numpy(), st=st.cpu().numpy(),
-             it=it.cpu().numpy())
     print("== done", np.unique(st.cpu().numpy(), return_counts=True))
+    ids = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else []
+    if ids:  # the warm answers of these instances (and their previous-tick answers)
+        np.savez(REPO / "gpurun_out" / "trace_warm_rows.npz", ids=np.array(ids),
+                 w=w[ids].cpu().numpy(), st=st[ids].cpu().numpy(), w_prev=w0[ids].cpu().numpy())
 
 
 if __name__ == "__main__":
