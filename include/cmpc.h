@@ -38,7 +38,11 @@
  *                                       a CERTIFIED bound on the force error of the held faces:
  *                                       with c = sum_f min(lambda_f, 0) a_f over the faces held,
  *                                       |u - u*|_2 <= |c|_2 / min(2R) <= 5e-5 x us (strong
- *                                       convexity).  Together: within ~1e-4 of the optimum.
+ *                                       convexity).  Together: within ~1e-4 of the optimum
+ *                                       except along directions weighed only by R, which the
+ *                                       fp32 refinement resolves poorly (fresh-seed surveys:
+ *                                       2 of 196,606 status-1 answers at 1.1e-4 / 2.1e-4,
+ *                                       DESIGN.md 8).
  *                                     2 solved inaccurate: ADMM residuals within eps, or a polished
  *                                       point that misses the certified bound (returned, but not
  *                                       verified to 1e-4),
