@@ -41,7 +41,8 @@
  *                                       convexity).  Together: within ~1e-4 of the optimum
  *                                       except along directions weighed only by R, which the
  *                                       fp32 refinement resolves poorly (fresh-seed surveys:
- *                                       2 of 196,606 status-1 answers at 1.1e-4 / 2.1e-4,
+ *                                       2 of 196,606 status-1 answers at 1.1e-4 / 2.1e-4 at
+ *                                       polish_refine 2, none above 5.6e-5 at polish_refine 4,
  *                                       DESIGN.md 8).
  *                                     2 solved inaccurate: ADMM residuals within eps, or a polished
  *                                       point that misses the certified bound (returned, but not
@@ -93,7 +94,8 @@ typedef struct cmpc_params {
   int32_t adaptive_rho_interval; /* iterations between rho updates (0 = off) */
   int32_t polish_stable;  /* polish after the active set is unchanged this many iterations */
   int32_t polish_refine;  /* refinement steps inside the polish before its convergence test may
-                             stop them (up to 4 more while the step still halves); default 2 */
+                             stop them (up to 4 more while the step still halves); default 2
+                             (4: ~5 % slower, tighter along R-weighted directions) */
   float polish_tol;       /* relative KKT tolerance for accepting the polished point */
   int32_t polish_repairs; /* active-set repairs (add violated / drop negative-multiplier faces
                              and re-polish) before resuming ADMM */
