@@ -170,3 +170,54 @@ def test_warm_primal_only_and_dual_only(plan):
         w2, st2, it2 = _solve(plan, d, **kw)
         assert np.all(st2.cpu().numpy() == 1)
         assert rel_err_U(w2.cpu().numpy(), fx["w"]).max() <= TOL_U
+
+
+# Fresh-seed warm tick (round 6, profiles/r06s_*, r06v_*): instances 31439 and 5794 of
+# synth.next_tick(make_batch(65536, 13, mixed)) warm from the previous tick are accepted at the
+# default polish_refine 2 with 2.1e-4 / 1.1e-4 error along directions weighed only by R
+# (DESIGN.md 8); polish_refine 4 brings them within the bar.  Each instance is solved
+# independently of the others (test_instance_order_independent), so the two, replicated past the
+# team bound (the one-wave kernels of the 65,536 batch), reproduce their in-batch answers.
+_FRESH_IDS = (31439, 5794)
+
+
+def _fresh_pair(reps=1100):
+    from cmpc import synth
+    prev = synth.make_batch(65536, 13, mixed=True)
+    nxt = synth.next_tick(prev)
+    keys = ("Ad", "Bd", "gd", "x0", "xref", "contact")
+    ids = np.repeat(np.array(_FRESH_IDS), reps)
+    return ({k: prev[k][ids] for k in keys}, {k: nxt[k][ids] for k in keys}, nxt)
+
+
+def _fresh_errors(polish_refine):
+    from cmpc import Plan, SolverParams
+    from oracle import mpc_qp, tight_solver
+    prev, nxt, full = _fresh_pair()
+    p = Plan(SolverParams(max_batch=len(prev["x0"]), polish_refine=polish_refine))
+    dp, dn = _dev(prev, p), _dev(nxt, p)
+    w0, _, _, y0 = _solve(p, dp, y_out=True)
+    w, st, it, _ = _solve(p, dn, w_init=w0, y_init=y0, y_out=True)
+    w, st = w.cpu().numpy(), st.cpu().numpy()
+    errs = []
+    for j, i in enumerate(_FRESH_IDS):
+        qp = mpc_qp.build_qp(full["Ad"][i], full["Bd"][i], full["gd"][i], full["x0"][i],
+                             full["xref"][i].T, full["contact"][i])
+        r = tight_solver.solve(qp)
+        assert max(r["kkt"].values()) < 1e-8
+        rows = slice(j * 1100, (j + 1) * 1100)
+        errs.append((st[rows], rel_err_U(w[rows], np.repeat(r["w"][None], 1100, axis=0))))
+    return errs
+
+
+def test_fresh_warm_tick_strict_setting():
+    """polish_refine 4: every status-1 answer of the two fresh-seed misses within 1e-4."""
+    for st, err in _fresh_errors(4):
+        assert np.all(err[st == 1] <= TOL_U), (np.unique(st), float(err.max()))
+
+
+@pytest.mark.xfail(reason="known gap at the default polish_refine 2: R-weighted directions "
+                          "(DESIGN.md 8)", strict=False)
+def test_fresh_warm_tick_default_setting():
+    for st, err in _fresh_errors(2):
+        assert np.all(err[st == 1] <= TOL_U), (np.unique(st), float(err.max()))
